@@ -1,0 +1,232 @@
+"""Benchmark: 6DOF env-steps/s of the fused HIP step at N envs per GPU (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ENVS_PER_GPU] [--model 6DOF|3DOF]
+                    [--allgather] [--no-graph] [--cpu-seconds S]
+
+A "step" = one launch of the fused step kernel over all N envs of a GPU: action in,
+RK4 rigid-body step + ground event + reward + done + obs + TimeLimit + auto-reset out.
+Inputs (a pool of 8 pre-generated U(-1,1) action batches, seeded) are resident in HBM
+before the timed region. Multi-GPU: one process per GPU (torchrun), env shards
+[rank*N, (rank+1)*N) with their own RNG streams; no data-path collective unless
+--allgather (RCCL all_gather of obs/reward/done after every step).
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Algorithmic HBM bytes per env-step: read state+action+v0, write
+# state+obs+reward+done.
+BYTES_PER_STEP = {6: 56 + 12 + 4 + 56 + 56 + 4 + 1, 3: 28 + 8 + 4 + 28 + 28 + 4 + 1}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+POOL = 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--n", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--model", default="6DOF")
+    ap.add_argument("--integrator", default="rk4")
+    ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-steps", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(model, seconds, seed=0):
+    """The CPU oracle (faithful scipy-RK45 restatement in C, 1 thread) stepping a
+    bounded sample of the same workload: envs from the same init_space, U(-1,1)
+    actions, auto-reset on done, TimeLimit 800."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    kw = O.ENV_CONFIG_6DOF if model == 6 else O.DEFAULTS_3DOF
+    cfg = O.make_cfg(model, **kw)
+    ns = 14 if model == 6 else 7
+    na = 3 if model == 6 else 2
+    if model == 6:
+        _, lo, hi, _, _ = O.derived6(**kw)
+    lo_ic = (np.float32(kw["IC"]) - np.float32(kw["ICRange"]) / 2).astype(np.float32)
+    hi_ic = (np.float32(kw["IC"]) + np.float32(kw["ICRange"]) / 2).astype(np.float32)
+    rng = np.random.default_rng(seed)
+    n = 1024
+
+    def sample(k):
+        ic = rng.uniform(lo_ic, hi_ic, (k, ns)).astype(np.float32)
+        if model == 6:
+            ic[:, 6:10] /= np.linalg.norm(ic[:, 6:10], axis=1, keepdims=True)
+        return ic
+
+    ic = sample(n)
+    s = ic.astype(np.float64)
+    el = np.zeros(n, np.int64)
+    t = np.zeros(n)
+    steps = 0
+    busy = 0.0
+    while busy < seconds:
+        a = rng.uniform(-1, 1, (n, na)).astype(np.float32)
+        t0 = time.perf_counter()
+        out = O.step(cfg, ic, t, s, a, nthreads=1)
+        busy += time.perf_counter() - t0
+        steps += n
+        s = out["state_out"]
+        t = np.round(t + cfg.dt, 3)
+        el += 1
+        d = out["done"] | (el >= 800)
+        if d.any():
+            k = int(d.sum())
+            ic[d] = sample(k)
+            s[d] = ic[d]
+            el[d] = 0
+            t[d] = 0
+    return {"value": steps / busy, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": "%d env-steps of %s (%d envs x %d steps, env_config ICs, U(-1,1) actions, auto-reset, "
+                      "TimeLimit 800) through oracle/librocket_oracle.so ro_step_batch, 1 thread; "
+                      "reference Python step() measured 569 (6DOF) / 3396 (3DOF) steps/s/core in the survey "
+                      "container (BASELINE.md)" % (steps, "6DOF" if model == 6 else "3DOF", n, steps // n)}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF, MAX_EPISODE_STEPS, parse_model
+
+    model = parse_model(args.model)
+    kw = ENV_CONFIG_6DOF if model == 6 else {}
+    n = args.n
+    env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
+                      episode_stats=False, integrator=args.integrator, env_id_offset=rank * n, **kw)
+    env.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(42 + rank)
+    pool = torch.rand((POOL, n, env.action_dim), device=dev, generator=gen) * 2 - 1
+    if args.allgather:
+        g_obs = torch.empty((world * n, env.state_dim), device=dev)
+        g_rew = torch.empty((world * n,), device=dev)
+        g_done = torch.empty((world * n,), device=dev, dtype=torch.uint8)
+
+    def one(k):
+        obs, rew, done, _ = env.step(pool[k % POOL])
+        if args.allgather and dist is not None:
+            dist.all_gather_into_tensor(g_obs, obs)
+            dist.all_gather_into_tensor(g_rew, rew)
+            dist.all_gather_into_tensor(g_done, done)
+
+    stream = torch.cuda.current_stream(dev)
+    for k in range(args.warmup):
+        one(k)
+    torch.cuda.synchronize(dev)
+
+    # ---- kernel duration: HIP events bracketing every launch (eager, same stream) ----
+    n_ev = min(200, max(20, args.steps // 10))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    for k, (e0, e1) in enumerate(evs):
+        e0.record(stream)
+        env.step(pool[k % POOL])
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    # ---- timed region: K steps (hipGraph replays of graph_steps launches each) ----
+    use_graph = not args.no_graph and not args.allgather
+    gs = args.graph_steps
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(stream)
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                for k in range(gs):
+                    env.step(pool[k % POOL])
+        stream.wait_stream(s)
+        torch.cuda.synchronize(dev)
+        graph.replay()  # warm the graph
+        torch.cuda.synchronize(dev)
+    K = args.steps
+    if use_graph:
+        K = max(gs, (K + gs - 1) // gs * gs)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if use_graph:
+        for _ in range(K // gs):
+            graph.replay()
+    else:
+        for k in range(K):
+            one(k)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    value = n * world * K / dt
+    bytes_launch = BYTES_PER_STEP[model] * n
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    result = {
+        "metric": "env-steps/sec (%s, N=%d per GPU)" % ("6DOF" if model == 6 else "3DOF", n),
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": dt / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: ICs ~ U(init_space of configuration_file.env_config), actions ~ U(-1,1) seeded pool of %d "
+                "batches resident in HBM" % POOL,
+        "config": {"workload": "Rocket%s N=%d per GPU, %s fused step+reward+TimeLimit(800)+auto-reset, %s"
+                               % ("6DOF" if model == 6 else "3DOF", n, args.integrator.upper(),
+                                  "RCCL all_gather of obs/reward/done each step" if args.allgather else
+                                  "no data-path collective"),
+                   "envs_per_gpu": n, "global_envs": n * world, "integrator": args.integrator,
+                   "graph_steps": gs if use_graph else 0,
+                   "parallelism": "env-sharded x%d" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "step_kernel<%d,%s>" % (model, args.integrator.upper()),
+                     "kernel_us": kern_ms * 1e3, "bytes_per_launch": bytes_launch,
+                     "bytes_per_env_step": BYTES_PER_STEP[model]},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(model, args.cpu_seconds)
+    env.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/*
+ * rocket_hip.h — C-ABI of librocket_hip.so, the MI355X-native vectorized
+ * rocket-landing env step (gfx950 HIP kernels).
+ *
+ * The reference has no native boundary: its hot path is the Python gym 0.21
+ * Env API (reference my_environment/envs/rocket_env.py). Each entry point below
+ * replaces one reference interface, batched over N independent envs that live in
+ * HBM in struct-of-arrays fp32 layout:
+ *
+ *   rr_create      <- Rocket6DOF.__init__ rocket_env.py:511-663 / Rocket.__init__ :27-135
+ *                     (kwargs lowered to rr_params on the host, rl_rocket_amd/params.py)
+ *   rr_reset       <- Rocket6DOF.reset rocket_env.py:665-688 / Rocket.reset :137-148
+ *                     (+ seed(): rocket_env.py:1063-1065 / :478-480)
+ *   rr_step        <- Rocket6DOF.step rocket_env.py:690-719 (+ Simulator6DOF.step/RHS
+ *                     simulator.py:227-378) / Rocket.step :150-175 (+ simulator.py:55-130),
+ *                     fused with gym TimeLimit (main_6DOF.py:67), the SB3 vec-env auto-reset
+ *                     and, optionally, RewardAnnealing (wrappers.py:68-86)
+ *   rr_set_state / rr_get_state
+ *                  <- direct access to Simulator*.state / .t used by the reference's
+ *                     callers (env.SIM, rocket_env.py:686, :694; used here for parity
+ *                     injection and checkpoint/restore)
+ *   rr_fetch_done / rr_copy_terminal / rr_get_buffers
+ *                  <- info["terminal_observation"] / Monitor episode stats for done envs
+ *                     (SB3 DummyVecEnv / Monitor around main_6DOF.py:64-70)
+ *
+ * Conventions
+ *   - All data pointers are DEVICE pointers (e.g. torch.Tensor.data_ptr()) on the
+ *     handle's device, owned by the caller unless stated otherwise.
+ *   - Every call is asynchronous on the given hipStream_t (pass as void*; NULL = the
+ *     default stream). Apart from rr_fetch_done (documented as synchronising), no call
+ *     synchronises, allocates or frees after rr_create, so rr_step / rr_reset can be
+ *     captured into a hipGraph (capture an even number of rr_step calls: the done list
+ *     is double-buffered by step parity).
+ *   - Return value: 0 on success, < 0 on error (RR_E*); rr_last_error() returns a
+ *     thread-local message. No exception or abort crosses the ABI.
+ *   - A handle is not thread-safe; use one handle per stream / GPU.
+ */
+#ifndef ROCKET_HIP_H
+#define ROCKET_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RR_ABI_VERSION 1
+
+/* error codes */
+#define RR_OK 0
+#define RR_EINVAL -1   /* bad argument */
+#define RR_EHIP -2     /* HIP runtime error */
+#define RR_ENOMEM -3   /* allocation failed */
+
+/* models */
+#define RR_MODEL_3DOF 3
+#define RR_MODEL_6DOF 6
+
+/* integrators. RK4 is the parity mode (matches the reference's adaptive RK45 +
+ * terminal ground event to <= 1e-5 floored-relative). EULER is a
+ * declared NON-parity speed mode (BASELINE config "3DOF Euler"). */
+#define RR_INT_RK4 0
+#define RR_INT_EULER 1
+
+/* rr_params.flags */
+#define RR_FLAG_AUTO_RESET 0x1        /* reset done envs inside rr_step (SB3 vec-env semantics) */
+#define RR_FLAG_EPISODE_STATS 0x2     /* keep per-env episode return (Monitor) */
+#define RR_FLAG_REWARD_ANNEALING 0x4  /* reward = attitude + goal - xi*(a_thrust+1)  (wrappers.py:72-86) */
+#define RR_FLAG_ACTION_SOA 0x8        /* action laid out [n_act][N] instead of [N][n_act] */
+
+#define RR_MAX_STATE 14
+
+/* Per-config constants. Lowered on the host from the reference env kwargs
+ * (rl_rocket_amd/params.py restates rocket_env.py:51-123 / :557-658). */
+typedef struct rr_params {
+    int32_t model;               /* RR_MODEL_3DOF | RR_MODEL_6DOF */
+    int32_t integrator;          /* RR_INT_* */
+    int32_t max_episode_steps;   /* gym TimeLimit; 0 = none */
+    uint32_t flags;              /* RR_FLAG_* */
+    float dt;                    /* timestep [s] */
+    float ic_low[RR_MAX_STATE];  /* init_space Box low  (float32, rocket_env.py:564-567) */
+    float ic_high[RR_MAX_STATE]; /* init_space Box high */
+    float normalizer[RR_MAX_STATE]; /* state_normalizer (rocket_env.py:592-612 / :76-94) */
+    float bounds_low[3];         /* 6DOF: position Box low; 3DOF: [-x_bound, -, -] */
+    float bounds_high[3];        /* 6DOF: position Box high; 3DOF: [x_bound, z_bound, -] */
+    float max_gimbal;            /* rad */
+    float max_thrust;            /* N */
+    float alfa, beta, eta, gamma, delta, kappa, xi; /* reward_coeff */
+    float waypoint, landing_radius, max_velocity;
+    float att_limit[3];          /* trajectory_limits["attitude_limit"] (zyx) */
+    float land_att_limit[3];     /* landing_params["landing_attitude_limit"] */
+    float omega_lim[3];          /* 0.2 hard-coded in the reference (rocket_env.py:656) */
+} rr_params;
+
+/* Library-owned device buffers, valid until rr_destroy. The done list refers to
+ * the MOST RECENT rr_step on the handle and is overwritten by the step after next
+ * (double-buffered): read it before issuing two more steps. */
+typedef struct rr_buffers {
+    float* state;          /* [state_dim][N] fp32 SoA */
+    float* v0;             /* [N] ||IC velocity|| of the episode (rocket_env.py:989-991) */
+    int32_t* elapsed;      /* [N] TimeLimit step counter */
+    float* ep_return;      /* [N] running episode return (RR_FLAG_EPISODE_STATS) */
+    int32_t* done_count;   /* [1] number of done envs in the last step */
+    int32_t* done_idx;     /* [N] their env indices (compacted by wave ballot, unordered) */
+    float* terminal_obs;   /* [N][state_dim] final obs of env i, valid where done[i] */
+    float* terminal_return;/* [N] episode return of env i, valid where done[i] */
+    int32_t* terminal_len; /* [N] episode length of env i, valid where done[i] */
+} rr_buffers;
+
+typedef struct rr_env rr_env;
+
+int rr_abi_version(void);
+const char* rr_last_error(void);
+
+/* Allocate N envs on `device`. env_id_offset = global id of env 0 (multi-GPU shards
+ * use rank*N so every env has its own RNG stream). Envs start un-initialised: call
+ * rr_reset before the first rr_step. */
+int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset, int device);
+int rr_destroy(rr_env* e);
+int64_t rr_num_envs(const rr_env* e);
+int rr_state_dim(const rr_env* e);
+int rr_action_dim(const rr_env* e);
+
+/* Re-seed every env's reset stream: seed + global env id (counter-free, deterministic). */
+int rr_seed(rr_env* e, uint64_t seed, void* stream);
+/* Sample a fresh initial condition for every env where mask[i] != 0 (all when mask is
+ * NULL), write the normalised obs [N][state_dim] (obs may be NULL). */
+int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream);
+
+/* One env step for all N envs.
+ *   action    [N][action_dim] fp32 normalised in [-1,1] (not clipped, like the reference)
+ *   obs       [N][state_dim] fp32 out (post-reset obs for done envs under AUTO_RESET)
+ *   reward    [N] fp32 out
+ *   done      [N] u8 out (ground event | bounds violation | TimeLimit)
+ *   truncated [N] u8 out or NULL (TimeLimit.truncated)
+ *   terms     [n_terms + 2][N] fp32 out or NULL: info["rewards_dict"] (6DOF 5 terms:
+ *             velocity_tracking, thrust_penalty, eta, attitude_constraint, rew_goal;
+ *             3DOF 6 terms: ..., attitude_hint, rew_goal), then two 0/1 planes:
+ *             info["bounds_violation"] and the ground event (solve_ivp status 1) */
+int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
+            float* terms, void* stream);
+
+/* Overwrite / read the per-env state (parity injection, checkpoint / restore).
+ * state_soa [state_dim][N] fp32; v0 [N] or NULL (then recomputed from nothing: kept);
+ * elapsed [N] or NULL (then zeroed on set / skipped on get). */
+int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32_t* elapsed, void* stream);
+int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void* stream);
+
+/* Pointers to the library-owned buffers (done list of the last step, etc.). */
+int rr_get_buffers(rr_env* e, rr_buffers* out);
+
+/* Host-side retrieval of the last step's done list (SB3 infos: terminal_observation,
+ * Monitor episode stats). SYNCHRONISES `stream`. Writes at most `capacity` rows into
+ * the HOST arrays (any may be NULL): idx [capacity], term_obs [capacity][state_dim],
+ * term_return [capacity], term_len [capacity]; rows are in ascending env order.
+ * Returns the number of done envs (>= 0) or an RR_E* code. */
+int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs, float* term_return,
+                      int32_t* term_len, void* stream);
+
+/* Device-to-device copy of the full per-env terminal buffers of the last step
+ * (rows valid where done[i]); any destination may be NULL. Asynchronous. */
+int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* term_len, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

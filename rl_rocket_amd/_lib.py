@@ -1,0 +1,133 @@
+"""ctypes bindings of ``librocket_hip.so`` (C-ABI declared in ``include/rocket_hip.h``).
+
+There is no CPU fallback: if the HIP library is missing, every entry point of the
+package raises.  ``torch`` is imported first so that the process has ONE HIP
+runtime (torch's bundled ``libamdhip64.so`` carries the same soname,
+``libamdhip64.so.7``, as the one ``librocket_hip.so`` links against; the dynamic
+loader reuses the already-loaded copy).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librocket_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
+
+ABI_VERSION = 1
+
+RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
+RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
+RR_INT_RK4, RR_INT_EULER = 0, 1
+RR_FLAG_AUTO_RESET = 0x1
+RR_FLAG_EPISODE_STATS = 0x2
+RR_FLAG_REWARD_ANNEALING = 0x4
+RR_FLAG_ACTION_SOA = 0x8
+RR_MAX_STATE = 14
+
+_f3 = ctypes.c_float * 3
+_f14 = ctypes.c_float * RR_MAX_STATE
+
+
+class RrParams(ctypes.Structure):
+    """Mirror of ``rr_params`` (include/rocket_hip.h)."""
+
+    _fields_ = [
+        ("model", ctypes.c_int32),
+        ("integrator", ctypes.c_int32),
+        ("max_episode_steps", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("dt", ctypes.c_float),
+        ("ic_low", _f14),
+        ("ic_high", _f14),
+        ("normalizer", _f14),
+        ("bounds_low", _f3),
+        ("bounds_high", _f3),
+        ("max_gimbal", ctypes.c_float),
+        ("max_thrust", ctypes.c_float),
+        ("alfa", ctypes.c_float),
+        ("beta", ctypes.c_float),
+        ("eta", ctypes.c_float),
+        ("gamma", ctypes.c_float),
+        ("delta", ctypes.c_float),
+        ("kappa", ctypes.c_float),
+        ("xi", ctypes.c_float),
+        ("waypoint", ctypes.c_float),
+        ("landing_radius", ctypes.c_float),
+        ("max_velocity", ctypes.c_float),
+        ("att_limit", _f3),
+        ("land_att_limit", _f3),
+        ("omega_lim", _f3),
+    ]
+
+
+class RrBuffers(ctypes.Structure):
+    """Mirror of ``rr_buffers``."""
+
+    _fields_ = [
+        ("state", ctypes.c_void_p),
+        ("v0", ctypes.c_void_p),
+        ("elapsed", ctypes.c_void_p),
+        ("ep_return", ctypes.c_void_p),
+        ("done_count", ctypes.c_void_p),
+        ("done_idx", ctypes.c_void_p),
+        ("terminal_obs", ctypes.c_void_p),
+        ("terminal_return", ctypes.c_void_p),
+        ("terminal_len", ctypes.c_void_p),
+    ]
+
+
+# symbol -> (restype, argtypes); the test suite checks this against include/rocket_hip.h
+_P = ctypes.c_void_p
+SIGNATURES = {
+    "rr_abi_version": (ctypes.c_int, []),
+    "rr_last_error": (ctypes.c_char_p, []),
+    "rr_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(RrParams), ctypes.c_int64, ctypes.c_int64,
+                                 ctypes.c_int]),
+    "rr_destroy": (ctypes.c_int, [_P]),
+    "rr_num_envs": (ctypes.c_int64, [_P]),
+    "rr_state_dim": (ctypes.c_int, [_P]),
+    "rr_action_dim": (ctypes.c_int, [_P]),
+    "rr_seed": (ctypes.c_int, [_P, ctypes.c_uint64, _P]),
+    "rr_reset": (ctypes.c_int, [_P, _P, _P, _P]),
+    "rr_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "rr_set_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "rr_get_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "rr_get_buffers": (ctypes.c_int, [_P, ctypes.POINTER(RrBuffers)]),
+    "rr_fetch_done": (ctypes.c_int64, [_P, ctypes.c_int64, _P, _P, _P, _P, _P]),
+    "rr_copy_terminal": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+}
+
+_LIB = None
+
+
+class RocketHipError(RuntimeError):
+    pass
+
+
+def load(require_torch=True):
+    """Load librocket_hip.so (raises if it has not been built: no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if require_torch:
+        import torch  # noqa: F401  (one HIP runtime per process, see module doc)
+    if not os.path.exists(LIB_PATH):
+        raise RocketHipError(
+            "librocket_hip.so is not built (expected at %s). Build it with "
+            "`python -m rl_rocket_amd.build` (hipcc, gfx950). There is no CPU fallback." % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.rr_abi_version() != ABI_VERSION:
+        raise RocketHipError("librocket_hip.so ABI %d != expected %d" % (lib.rr_abi_version(), ABI_VERSION))
+    _LIB = lib
+    return lib
+
+
+def check(rc, what="rocket_hip"):
+    if rc < 0:
+        msg = load().rr_last_error()
+        raise RocketHipError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+    return rc

@@ -1,0 +1,146 @@
+"""``RocketBatch``: N rocket envs on one GPU behind the C-ABI, torch tensors in and out.
+
+This is the device-resident core that both the SB3-style ``RocketVecEnv`` and the
+single-env gym shims (``Rocket6DOF`` / ``Rocket``) sit on.  Every method launches
+asynchronously on the current torch stream of the env's device; nothing here
+synchronises except ``fetch_done``.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .params import lower, make_config
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class RocketBatch:
+    def __init__(self, num_envs, model="6DOF", device=None, max_episode_steps=0, auto_reset=True,
+                 episode_stats=True, reward_annealing=False, integrator="rk4", env_id_offset=0,
+                 compute_terms=False, seed=None, **env_kwargs):
+        import torch
+
+        self.torch = torch
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError("RocketBatch runs on a GPU (HIP) device; got %s — there is no CPU fallback" % device)
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.cfg = make_config(model, **env_kwargs)
+        self.model = self.cfg.model
+        self.num_envs = int(num_envs)
+        self.state_dim = self.cfg.state_dim
+        self.action_dim = self.cfg.action_dim
+        self.n_terms = len(self.cfg.term_names)
+        self.params = lower(self.cfg, max_episode_steps=max_episode_steps, auto_reset=auto_reset,
+                            episode_stats=episode_stats, reward_annealing=reward_annealing, integrator=integrator)
+        self.lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.rr_create(ctypes.byref(h), ctypes.byref(self.params), self.num_envs, int(env_id_offset),
+                                      device.index), "rr_create")
+        self._h = h
+        n, ns = self.num_envs, self.state_dim
+        kw = dict(device=device)
+        self.obs = torch.empty((n, ns), dtype=torch.float32, **kw)
+        self.reward = torch.empty((n,), dtype=torch.float32, **kw)
+        self.done = torch.empty((n,), dtype=torch.uint8, **kw)
+        self.truncated = torch.empty((n,), dtype=torch.uint8, **kw)
+        self.terms = torch.empty((self.n_terms + 2, n), dtype=torch.float32, **kw) if compute_terms else None
+        self.seed(self.cfg.kwargs["seed"] if seed is None else seed)
+
+    # -- plumbing ---------------------------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check_action(self, action):
+        t = self.torch
+        if not isinstance(action, t.Tensor):
+            action = t.as_tensor(np.asarray(action, dtype=np.float32), device=self.device)
+        if action.device != self.device:
+            action = action.to(self.device, non_blocking=True)
+        if action.dtype != t.float32:
+            action = action.float()
+        action = action.reshape(self.num_envs, self.action_dim)
+        if not action.is_contiguous():
+            action = action.contiguous()
+        return action
+
+    # -- API --------------------------------------------------------------------------------------------------
+    def seed(self, seed):
+        _lib.check(self.lib.rr_seed(self._h, int(seed) & (2 ** 64 - 1), self._stream()), "rr_seed")
+
+    def reset(self, mask=None):
+        m = None
+        if mask is not None:
+            m = self.torch.as_tensor(mask, device=self.device).to(self.torch.uint8).contiguous()
+        _lib.check(self.lib.rr_reset(self._h, _ptr(m), _ptr(self.obs), self._stream()), "rr_reset")
+        return self.obs
+
+    def step(self, action):
+        """One env step for all envs. Returns the (reused) output tensors
+        (obs [N,ns], reward [N], done [N] u8, truncated [N] u8)."""
+        action = self._check_action(action)
+        self._last_action = action  # keep alive until the kernel has run
+        _lib.check(self.lib.rr_step(self._h, _ptr(action), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                                    _ptr(self.truncated), _ptr(self.terms), self._stream()), "rr_step")
+        return self.obs, self.reward, self.done, self.truncated
+
+    def set_state(self, state_soa, v0=None, elapsed=None):
+        t = self.torch
+        st = t.as_tensor(state_soa, device=self.device, dtype=t.float32).reshape(self.state_dim, self.num_envs)
+        st = st.contiguous()
+        v = None if v0 is None else t.as_tensor(v0, device=self.device, dtype=t.float32).reshape(-1).contiguous()
+        el = None if elapsed is None else t.as_tensor(elapsed, device=self.device, dtype=t.int32).reshape(-1).contiguous()
+        self._keep = (st, v, el)
+        _lib.check(self.lib.rr_set_state(self._h, _ptr(st), _ptr(v), _ptr(el), self._stream()), "rr_set_state")
+
+    def get_state(self):
+        t = self.torch
+        st = t.empty((self.state_dim, self.num_envs), dtype=t.float32, device=self.device)
+        v = t.empty((self.num_envs,), dtype=t.float32, device=self.device)
+        el = t.empty((self.num_envs,), dtype=t.int32, device=self.device)
+        _lib.check(self.lib.rr_get_state(self._h, _ptr(st), _ptr(v), _ptr(el), self._stream()), "rr_get_state")
+        return st, v, el
+
+    def fetch_done(self, capacity=None):
+        """Done list of the last step on the host: (idx, terminal_obs, episode_return, episode_len).
+        Synchronises the stream."""
+        cap = self.num_envs if capacity is None else int(capacity)
+        idx = np.empty(cap, np.int32)
+        tobs = np.empty((cap, self.state_dim), np.float32)
+        ret = np.empty(cap, np.float32)
+        ln = np.empty(cap, np.int32)
+        c = self.lib.rr_fetch_done(self._h, cap, idx.ctypes.data_as(ctypes.c_void_p),
+                                   tobs.ctypes.data_as(ctypes.c_void_p), ret.ctypes.data_as(ctypes.c_void_p),
+                                   ln.ctypes.data_as(ctypes.c_void_p), self._stream())
+        _lib.check(c, "rr_fetch_done")
+        m = min(int(c), cap)
+        return idx[:m], tobs[:m], ret[:m], ln[:m]
+
+    def copy_terminal(self):
+        """Device copies of the per-env terminal buffers (rows valid where done)."""
+        t = self.torch
+        tobs = t.empty((self.num_envs, self.state_dim), dtype=t.float32, device=self.device)
+        ret = t.empty((self.num_envs,), dtype=t.float32, device=self.device)
+        ln = t.empty((self.num_envs,), dtype=t.int32, device=self.device)
+        _lib.check(self.lib.rr_copy_terminal(self._h, _ptr(tobs), _ptr(ret), _ptr(ln), self._stream()),
+                   "rr_copy_terminal")
+        return tobs, ret, ln
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.torch.cuda.synchronize(self.device)
+            self.lib.rr_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,51 @@
+"""Build ``librocket_hip.so`` in-tree with hipcc for gfx950 (MI355X).
+
+    python -m rl_rocket_amd.build [--force] [--resource-usage]
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "rocket_hip.hip")
+HEADER = os.path.join(ROOT, "include", "rocket_hip.h")
+OUT = os.path.join(HERE, "librocket_hip.so")
+ARCH = os.environ.get("RR_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def command(resource_usage=False):
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(ROOT, "include"), "-o", OUT, SRC]
+    if resource_usage:
+        cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
+    return cmd
+
+
+def up_to_date():
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(p) <= t for p in (SRC, HEADER, __file__))
+
+
+def build(force=False, resource_usage=False, verbose=True):
+    if not force and up_to_date():
+        return OUT
+    cmd = command(resource_usage)
+    if verbose:
+        print("[rl_rocket_amd.build]", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd, cwd=ROOT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, resource_usage="--resource-usage" in sys.argv)

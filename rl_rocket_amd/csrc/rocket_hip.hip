@@ -1,0 +1,1011 @@
+// rocket_hip.hip — MI355X (gfx950) kernels and C-ABI for the vectorized rocket env.
+//
+// One lane = one env. The per-env state lives in HBM as fp32 struct-of-arrays
+// planes ([state_dim][N]); one launch of step_kernel does, for every env:
+//   action denormalisation   (rocket_env.py:969-981 / :395-406)
+//   RK4 integration of the rigid-body ODE over dt with the terminal ground event
+//                            (simulator.py:227-294 / :55-130; the reference uses
+//                             scipy RK45 + brentq on its dense output)
+//   quaternion renormalisation / theta wrap (simulator.py:250 / :77)
+//   bounds check, reward shaping, landing check, obs normalisation
+//                            (rocket_env.py:690-719, 825-859, 963-1061 / :150-247, 431-476)
+//   TimeLimit, auto-reset with an in-kernel RNG, done compaction by wave ballot
+// with state kept in registers, the [N][state_dim] observation tile staged through
+// LDS so that it leaves the CU as 16-byte coalesced stores.
+//
+// Element-wise ODE work: no contraction, so no MFMA. The roofline is HBM bytes
+// (189 B per 6DOF env-step, 101 B per 3DOF env-step).
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rocket_hip.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// ---------------------------------------------------------------------------
+// Physical constants of the reference simulators.
+//   6DOF: simulator.py:210-224 — g0 9.81, Isp 360, J = diag(75350.25, 6037675.13,
+//         6037675.13), thrust hinge r_T_B = [-15, 0, 0], aero force identically 0.
+//   3DOF: simulator.py:36-51, :100-126 — rho 1.225, Cd 0.3, Sref 10.5, alpha = 0
+//         (normal force 0), I 6.04e6, lever x_T - x_CG = 30.
+// ---------------------------------------------------------------------------
+constexpr float kG0 = 9.81f;
+constexpr double kIsp = 360.0;
+constexpr double kJ1 = 75350.25, kJ2 = 6037675.13, kJ3 = 6037675.13;
+constexpr double kRT = -15.0;
+constexpr double kDrag3 = 0.5 * 1.225 * 0.3 * 10.5;  // A = Cd * (0.5 rho v^2) * Sref
+constexpr double kLever3 = 40.0 - 10.0;               // x_T - x_CG
+constexpr double kI3 = 6.04e6;
+
+// Device-side constants, derived once on the host from rr_params (see make_kparams).
+struct KParams {
+    int32_t max_steps;
+    uint32_t flags;
+    float h, h2, h6;          // dt, dt/2, dt/6
+    float ic_low[RR_MAX_STATE];
+    float ic_span[RR_MAX_STATE];
+    float inv_norm[RR_MAX_STATE];
+    float blo[3], bhi[3];     // 6DOF: inclusive position box; 3DOF: x_lo(<=), x_hi(>=), z_hi(>=)
+    float max_gimbal, half_thrust;
+    float alfa, beta, eta, gamma, delta, kappa, xi;
+    float waypoint, land_r2, land_v2;
+    // attitude tests on the zyx Euler angles without inverse trig (make_kparams):
+    //   |atan2(Y,X)| > L  <=>  X < r cos L ;  |asin(S)| > L  <=>  |S| > sin L
+    float att_c[3];           // threshold per axis for "> limit"
+    float land_c[3];          // threshold per axis for "< limit"
+    uint32_t att_never;       // bit k: "|e_k| > limit" can never hold
+    uint32_t land_always;     // bit k: "|e_k| < limit" always holds
+    float omega_lt;           // |w| < omega_lim  (float threshold, reference 0.2)
+    float zero_h;             // x <= 1e-3 as a float threshold
+    float dm;                 // -1/(g0*Isp) scale: dm = T * dm
+    // 6DOF rotational constants
+    float jinv[3], jd[3];     // 1/J_i and (J3-J2, J1-J3, J2-J1)
+    float rt15;               // -r_T_B x  -> tau = [0, 15 Tbz, -15 Tby]
+    // 3DOF
+    float drag3, lever_over_i3, zeta_hint;  // zeta_hint = pi/2
+};
+
+struct Bufs {
+    float* state;
+    float* v0;
+    int32_t* elapsed;
+    uint32_t* rng;            // [N][4] xoshiro128+ state
+    float* ep_ret;
+    int32_t* done_count;      // [2]
+    int32_t* done_idx;
+    float* term_obs;
+    float* term_ret;
+    int32_t* term_len;
+    int64_t n;
+    int64_t id_off;
+};
+
+struct StepIO {
+    const float* action;
+    float* obs;
+    float* reward;
+    uint8_t* done;
+    uint8_t* truncated;
+    float* terms;
+    int32_t parity;
+    int32_t obs_vec_ok;       // obs pointer 16-B aligned: LDS-staged float4 stores
+};
+
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+
+// ---------------------------------------------------------------------------
+// xoshiro128+ per-env reset stream (16 B of state, touched only on reset).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+
+struct Rng {
+    uint32_t s0, s1, s2, s3;
+    __device__ __forceinline__ float uniform()
+    {
+        uint32_t r = s0 + s3;
+        uint32_t t = s1 << 9;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl32(s3, 11);
+        return (float)(r >> 8) * 0x1p-24f;  // [0, 1), 24 random bits
+    }
+};
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t& x)
+{
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// ---------------------------------------------------------------------------
+// Model traits
+// ---------------------------------------------------------------------------
+template <int MODEL>
+struct Dims;
+template <>
+struct Dims<6> {
+    static constexpr int NS = 14, NA = 3, NT = 5, EV = 0;  // event on x (altitude)
+};
+template <>
+struct Dims<3> {
+    static constexpr int NS = 7, NA = 2, NT = 6, EV = 1;   // event on z (altitude)
+};
+
+// Controls, fixed over one env step.
+struct Ctl {
+    // 6DOF: body-frame thrust T_b = T [cy cz, sy cz, sz] (simulator.py:311-318, :350-357)
+    float tbx, tby, tbz;
+    float tau1, tau2;       // r_T_B x T_b (simulator.py:373-378), component 0 is 0
+    // 3DOF
+    float sd, cd, thrust, dom;
+    float dm;               // -T/(g0 Isp)
+};
+
+template <int MODEL>
+__device__ __forceinline__ Ctl make_ctl(const KParams& P, const float* a)
+{
+    Ctl c;
+    if constexpr (MODEL == 6) {
+        float dy = a[0] * P.max_gimbal, dz = a[1] * P.max_gimbal;
+        float T = (a[2] + 1.0f) * P.half_thrust;
+        float cy = __cosf(dy), sy = __sinf(dy), cz = __cosf(dz), sz = __sinf(dz);
+        c.tbx = T * (cy * cz);
+        c.tby = T * (sy * cz);
+        c.tbz = T * sz;
+        c.tau1 = P.rt15 * c.tbz;
+        c.tau2 = -P.rt15 * c.tby;
+        c.dm = T * P.dm;
+    } else {
+        float d = a[0] * P.max_gimbal;
+        float T = (a[1] + 1.0f) * P.half_thrust;
+        c.sd = __sinf(d);
+        c.cd = __cosf(d);
+        c.thrust = T;
+        c.dom = -(T * c.sd) * P.lever_over_i3;
+        c.dm = T * P.dm;
+    }
+    return c;
+}
+
+// 6DOF RHS, simulator.py:259-294. R(q/|q|) T_b is applied as a quaternion rotation
+// (t = 2 u x T_b; F = T_b + w t + u x t) — the same rotation as scipy's as_matrix().
+template <int MODEL>
+__device__ __forceinline__ void rhs(const KParams& P, const Ctl& c, const float* s, float* d)
+{
+    if constexpr (MODEL == 6) {
+        const float q0 = s[6], q1 = s[7], q2 = s[8], q3 = s[9];
+        const float w1 = s[10], w2 = s[11], w3 = s[12];
+        float rn = frsq(q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3);
+        float w = q0 * rn, ux = q1 * rn, uy = q2 * rn, uz = q3 * rn;
+        float tx = 2.0f * (uy * c.tbz - uz * c.tby);
+        float ty = 2.0f * (uz * c.tbx - ux * c.tbz);
+        float tz = 2.0f * (ux * c.tby - uy * c.tbx);
+        float Fx = c.tbx + w * tx + (uy * tz - uz * ty);
+        float Fy = c.tby + w * ty + (uz * tx - ux * tz);
+        float Fz = c.tbz + w * tz + (ux * ty - uy * tx);
+        float im = frcp(s[13]);
+        d[0] = s[3];
+        d[1] = s[4];
+        d[2] = s[5];
+        d[3] = Fx * im - kG0;
+        d[4] = Fy * im;
+        d[5] = Fz * im;
+        // dq = 0.5 Omega(w) q with the unnormalised q (simulator.py:287, :362-370)
+        d[6] = 0.5f * (-w1 * q1 - w2 * q2 - w3 * q3);
+        d[7] = 0.5f * (w1 * q0 + w3 * q2 - w2 * q3);
+        d[8] = 0.5f * (w2 * q0 - w3 * q1 + w1 * q3);
+        d[9] = 0.5f * (w3 * q0 + w2 * q1 - w1 * q2);
+        // dw = J^-1 (tau - w x Jw) (simulator.py:288)
+        d[10] = P.jinv[0] * (-(P.jd[0] * (w2 * w3)));
+        d[11] = P.jinv[1] * (c.tau1 - P.jd[1] * (w1 * w3));
+        d[12] = P.jinv[2] * (c.tau2 - P.jd[2] * (w1 * w2));
+        d[13] = c.dm;
+    } else {
+        // 3DOF RHS, simulator.py:88-130 (N = 0; the z-drag uses cos(phi): reference quirk)
+        const float th = s[2], vx = s[3], vz = s[4];
+        float st = __sinf(th), ct = __cosf(th);
+        float A = P.drag3 * (vx * vx + vz * vz);
+        float cdt = c.cd * ct - c.sd * st;   // cos(delta + phi)
+        float sdt = c.sd * ct + c.cd * st;   // sin(delta + phi)
+        float im = frcp(s[6]);
+        d[0] = vx;
+        d[1] = vz;
+        d[2] = s[5];
+        d[3] = (c.thrust * cdt - A * ct) * im;
+        d[4] = (c.thrust * sdt - A * ct) * im - kG0;
+        d[5] = c.dom;
+        d[6] = c.dm;
+    }
+}
+
+template <int MODEL, int INTEG>
+__device__ __forceinline__ void integrate(const KParams& P, const Ctl& c, const float* y0, float h,
+                                          float* y1, float* f0)
+{
+    constexpr int NS = Dims<MODEL>::NS;
+    float k[NS], yt[NS];
+    if constexpr (INTEG == RR_INT_EULER) {
+        rhs<MODEL>(P, c, y0, k);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            f0[j] = k[j];
+            y1[j] = y0[j] + h * k[j];
+        }
+    } else {
+        const float hh = 0.5f * h, h6 = h * (1.0f / 6.0f);
+        float acc[NS];
+        rhs<MODEL>(P, c, y0, k);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            f0[j] = k[j];
+            acc[j] = k[j];
+            yt[j] = y0[j] + hh * k[j];
+        }
+        rhs<MODEL>(P, c, yt, k);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            acc[j] += 2.0f * k[j];
+            yt[j] = y0[j] + hh * k[j];
+        }
+        rhs<MODEL>(P, c, yt, k);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            acc[j] += 2.0f * k[j];
+            yt[j] = y0[j] + h * k[j];
+        }
+        rhs<MODEL>(P, c, yt, k);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) y1[j] = y0[j] + h6 * (acc[j] + k[j]);
+    }
+}
+
+// Terminal ground event (solve_ivp events=..., terminal, direction 0; scipy
+// ivp.find_active_events): sign change of the altitude between the step ends.
+// The reference returns its dense output at the brentq root; here the root of the
+// cubic Hermite interpolant of the altitude (values and exact derivatives dx/dt = v
+// at both ends) is found by safeguarded Newton, and the state is re-integrated from
+// y0 to that time.
+template <int MODEL, int INTEG>
+__device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const float* y0, const float* f0,
+                                        float* y1)
+{
+    constexpr int EV = Dims<MODEL>::EV;
+    constexpr int NS = Dims<MODEL>::NS;
+    const float x0 = y0[EV], x1 = y1[EV];
+    float s;
+    if (x0 == 0.0f) {
+        s = 0.0f;
+    } else if (x1 == 0.0f) {
+        return;  // root at the step end: state unchanged
+    } else {
+        const float hv0 = P.h * f0[EV];          // h * dx/dt(0)
+        const float hv1 = P.h * y1[EV + 3];      // h * dx/dt(1) = h * v_alt(1)
+        float lo = 0.0f, hi = 1.0f;              // H(lo) has the sign of x0
+        s = x0 / (x0 - x1);
+        for (int it = 0; it < 12; ++it) {
+            float s2 = s * s, s3 = s2 * s;
+            float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
+                      (s3 - s2) * hv1;
+            float dH = (6 * s2 - 6 * s) * (x0 - x1) + (3 * s2 - 4 * s + 1) * hv0 + (3 * s2 - 2 * s) * hv1;
+            if (H == 0.0f) break;
+            if ((H > 0.0f) == (x0 > 0.0f)) lo = s;
+            else hi = s;
+            float sn = s - H / dH;
+            if (!(sn > lo && sn < hi)) sn = 0.5f * (lo + hi);
+            if (fabsf(sn - s) < 1e-7f) {
+                s = sn;
+                break;
+            }
+            s = sn;
+        }
+    }
+    float f_unused[NS];
+    integrate<MODEL, INTEG>(P, c, y0, s * P.h, y1, f_unused);
+}
+
+// Sample one initial condition: gym Box.sample (uniform in [low, high], float32),
+// then q <- q/|q| (rocket_env.py:672-673); v0 = |IC velocity| (rocket_env.py:989-991).
+template <int MODEL>
+__device__ __forceinline__ void sample_ic(const KParams& P, Rng& g, float* s, float& v0)
+{
+    constexpr int NS = Dims<MODEL>::NS;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) s[j] = fmaf(P.ic_span[j], g.uniform(), P.ic_low[j]);
+    if constexpr (MODEL == 6) {
+        float nq = sqrtf(s[6] * s[6] + s[7] * s[7] + s[8] * s[8] + s[9] * s[9]);
+        s[6] /= nq;
+        s[7] /= nq;
+        s[8] /= nq;
+        s[9] /= nq;
+        v0 = sqrtf(s[3] * s[3] + s[4] * s[4] + s[5] * s[5]);
+    } else {
+        v0 = sqrtf(s[3] * s[3] + s[4] * s[4]);
+    }
+}
+
+// Reward / done of the reference env on the float32 post-step state.
+template <int MODEL>
+__device__ __forceinline__ float reward_terms(const KParams& P, const float* s, const float* a, float v0,
+                                              bool& bounds_violation, float* t)
+{
+    if constexpr (MODEL == 6) {
+        // _check_bounds_violation: Box(lo, hi, float32).contains(r) (rocket_env.py:1036-1038)
+        bool inside = s[0] >= P.blo[0] && s[0] <= P.bhi[0] && s[1] >= P.blo[1] && s[1] <= P.bhi[1] &&
+                      s[2] >= P.blo[2] && s[2] <= P.bhi[2];
+        bounds_violation = !inside;
+        // _compute_vtarg (rocket_env.py:986-1014)
+        float rh0, rh1, rh2, vh0, tau_inv;
+        if (s[0] > P.waypoint) {
+            rh0 = s[0] - P.waypoint; rh1 = s[1]; rh2 = s[2];
+            vh0 = s[3] + 2.0f;
+            tau_inv = 1.0f / 20.0f;
+        } else {
+            rh0 = s[0] + 1.0f; rh1 = 0.0f; rh2 = 0.0f;
+            vh0 = s[3] + 1.0f;
+            tau_inv = 1.0f / 100.0f;
+        }
+        float nrh = sqrtf(rh0 * rh0 + rh1 * rh1 + rh2 * rh2);
+        float nvh = sqrtf(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
+        float t_go = nrh / nvh;
+        float f = (-v0 / fmaxf(1e-3f, nrh)) * (-expm1f(-t_go * tau_inv));
+        float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
+        t[0] = P.alfa * sqrtf(e0 * e0 + e1 * e1 + e2 * e2);
+        // thrust_penalty = beta * T (denormalised, float32)
+        t[1] = P.beta * ((a[2] + 1.0f) * P.half_thrust);
+        t[2] = P.eta;
+        // zyx Euler angles of q (Rotation.as_euler("zyx"), rocket_env.py:852-855, 1047):
+        //   a = atan2(-R01, R00), b = asin(R02), c = atan2(-R12, R22)
+        const float w = s[6], x = s[7], y = s[8], z = s[9];
+        float qq = w * w + x * x + y * y + z * z;
+        float R00 = w * w + x * x - y * y - z * z;
+        float mR01 = 2.0f * (z * w - x * y);
+        float R02 = 2.0f * (x * z + y * w);
+        float mR12 = 2.0f * (x * w - y * z);
+        float R22 = w * w - x * x - y * y + z * z;
+        float ra = sqrtf(R00 * R00 + mR01 * mR01);
+        float rc = sqrtf(R22 * R22 + mR12 * mR12);
+        float sb = fabsf(R02) / qq;
+        bool att = (!(P.att_never & 1u) && R00 < ra * P.att_c[0]) || (!(P.att_never & 2u) && sb > P.att_c[1]) ||
+                   (!(P.att_never & 4u) && R22 < rc * P.att_c[2]);
+        t[3] = att ? P.gamma : 0.0f;
+        // _check_landing (rocket_env.py:1040-1061); any() over angles and omega is the reference's
+        bool att_ok = (P.land_always & 1u) || R00 > ra * P.land_c[0] || (P.land_always & 2u) ||
+                      sb < P.land_c[1] || (P.land_always & 4u) || R22 > rc * P.land_c[2];
+        bool om_ok = fabsf(s[10]) < P.omega_lt || fabsf(s[11]) < P.omega_lt || fabsf(s[12]) < P.omega_lt;
+        float r2 = s[0] * s[0] + s[1] * s[1] + s[2] * s[2];
+        float v2 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
+        bool landing = s[0] <= P.zero_h && v2 < P.land_v2 && r2 < P.land_r2 && att_ok && om_ok;
+        t[4] = landing ? P.kappa : 0.0f;
+        if (P.flags & RR_FLAG_REWARD_ANNEALING) return t[3] + t[4] - P.xi * (a[2] + 1.0f);
+        return t[0] + t[1] + t[2] + t[3] + t[4] + (bounds_violation ? -50.0f : 0.0f);
+    } else {
+        // _check_bounds (rocket_env.py:431-447)
+        bounds_violation = s[0] <= P.blo[0] || s[0] >= P.bhi[0] || s[1] >= P.bhi[1];
+        // _compute_vtarg (rocket_env.py:219-247)
+        float rh0, rh1, vh1, tau_inv;
+        if (s[1] > P.waypoint) {
+            rh0 = s[0]; rh1 = s[1] - P.waypoint;
+            vh1 = s[4] + 2.0f;
+            tau_inv = 1.0f / 20.0f;
+        } else {
+            rh0 = 0.0f; rh1 = s[1];
+            vh1 = s[4] + 1.0f;
+            tau_inv = 1.0f / 100.0f;
+        }
+        float nrh = sqrtf(rh0 * rh0 + rh1 * rh1);
+        float nvh = sqrtf(s[3] * s[3] + vh1 * vh1);
+        float t_go = nrh / nvh;
+        float f = (-v0 / fmaxf(1e-3f, nrh)) * (-expm1f(-t_go * tau_inv));
+        float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1;
+        t[0] = P.alfa * sqrtf(e0 * e0 + e1 * e1);
+        t[1] = P.beta * ((a[1] + 1.0f) * P.half_thrust);
+        t[2] = P.eta;
+        float zeta = fabsf(s[2] - P.zeta_hint);
+        t[3] = zeta > 2.0f * 3.14159265358979f ? P.gamma : 0.0f;
+        t[4] = P.delta * fmaxf(0.0f, zeta - P.zeta_hint);
+        // _check_landing (rocket_env.py:449-476)
+        float r2 = s[0] * s[0] + s[1] * s[1];
+        float v2 = s[3] * s[3] + s[4] * s[4];
+        bool landing = s[1] <= P.zero_h && v2 < P.land_v2 && r2 < P.land_r2 && zeta < 0.2f &&
+                       fabsf(s[5]) < P.omega_lt;
+        t[5] = landing ? P.kappa : 0.0f;
+        if (P.flags & RR_FLAG_REWARD_ANNEALING) return t[3] + t[5] - P.xi * (a[1] + 1.0f);
+        return t[0] + t[1] + t[2] + t[3] + t[4] + t[5] + (bounds_violation ? -50.0f : 0.0f);
+    }
+}
+
+// Write this wave's [64][NS] observation tile through LDS as 16-B coalesced stores.
+template <int NS>
+__device__ __forceinline__ void store_obs_tile(float* lds, const float* o, float* obs, int64_t wave_base,
+                                               int lane, int64_t n, bool vec_ok)
+{
+#pragma unroll
+    for (int j = 0; j < NS; ++j) lds[lane * NS + j] = o[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t nvalid = (n - wave_base) < kWave ? (n - wave_base) : kWave;
+    float* dst = obs + wave_base * NS;
+    if (vec_ok && nvalid == kWave) {
+        constexpr int NV = kWave * NS / 4;
+        const float4* src4 = reinterpret_cast<const float4*>(lds);
+        float4* dst4 = reinterpret_cast<float4*>(dst);
+#pragma unroll
+        for (int k = lane; k < NV; k += kWave) dst4[k] = src4[k];
+    } else {
+        const int tot = (int)nvalid * NS;
+        for (int k = lane; k < tot; k += kWave) dst[k] = lds[k];
+    }
+}
+
+template <int MODEL, int INTEG>
+__global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Bufs B, const StepIO io)
+{
+    constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
+    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][kWave * NS];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int64_t n = B.n;
+    const int64_t wave_base = (int64_t)blockIdx.x * kBlock + (int64_t)wv * kWave;
+    if (blockIdx.x == 0 && threadIdx.x == 0) B.done_count[io.parity ^ 1] = 0;  // next step's list
+    if (wave_base >= n) return;  // wave-uniform
+    const int64_t i = wave_base + lane;
+    const bool valid = i < n;
+    const int64_t ic = valid ? i : n - 1;
+
+    float y0[NS], y1[NS], f0[NS], a[NA];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) y0[j] = B.state[(int64_t)j * n + ic];
+    if (P.flags & RR_FLAG_ACTION_SOA) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) a[j] = io.action[(int64_t)j * n + ic];
+    } else {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) a[j] = io.action[ic * NA + j];
+    }
+    float v0 = B.v0[ic];
+
+    const Ctl c = make_ctl<MODEL>(P, a);
+    integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
+    const float g0 = y0[EV], g1 = y1[EV];
+    const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
+    if (event) event_step<MODEL, INTEG>(P, c, y0, f0, y1);
+
+    if constexpr (MODEL == 6) {
+        // _normalize_quaternion (simulator.py:250)
+        float rn = frsq(y1[6] * y1[6] + y1[7] * y1[7] + y1[8] * y1[8] + y1[9] * y1[9]);
+        y1[6] *= rn;
+        y1[7] *= rn;
+        y1[8] *= rn;
+        y1[9] *= rn;
+    } else {
+        // _wrapTo2Pi (simulator.py:150-163): fmod(fmod(theta, 2pi) + 2pi, 2pi)
+        const float two_pi = 6.28318530717958647692f;
+        float th = fmodf(y1[2], two_pi) + two_pi;
+        y1[2] = fmodf(th, two_pi);
+    }
+
+    bool bv;
+    float t[NT];
+    float r = reward_terms<MODEL>(P, y1, a, v0, bv, t);
+    bool done = event || bv;
+
+    // gym TimeLimit (main_6DOF.py:67): elapsed += 1; at the limit done = True and
+    // info["TimeLimit.truncated"] = not done
+    bool trunc = false;
+    int32_t el = 0;
+    if (P.max_steps > 0 || (P.flags & RR_FLAG_EPISODE_STATS)) {
+        el = B.elapsed[ic] + 1;
+        if (P.max_steps > 0 && el >= P.max_steps) {
+            trunc = !done;
+            done = true;
+        }
+    }
+    float ret = 0.0f;
+    if (P.flags & RR_FLAG_EPISODE_STATS) ret = B.ep_ret[ic] + r;
+
+    float o[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) o[j] = y1[j] * P.inv_norm[j];
+
+    // Done compaction: one ballot per wave, one atomic per wave with any done lane.
+    const bool dv = done && valid;
+    const uint64_t m = __ballot(dv);
+    if (m) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&B.done_count[io.parity], __popcll(m));
+        base = __shfl(base, 0);
+        if (dv) {
+            const int rank = __popcll(m & ((1ull << lane) - 1ull));
+            B.done_idx[base + rank] = (int32_t)i;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) B.term_obs[i * NS + j] = o[j];
+            B.term_ret[i] = ret;
+            B.term_len[i] = el;
+        }
+        if ((P.flags & RR_FLAG_AUTO_RESET) && dv) {
+            uint4* rs = reinterpret_cast<uint4*>(B.rng) + i;
+            uint4 st = *rs;
+            Rng g{st.x, st.y, st.z, st.w};
+            sample_ic<MODEL>(P, g, y1, v0);
+            *rs = make_uint4(g.s0, g.s1, g.s2, g.s3);
+            B.v0[i] = v0;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) o[j] = y1[j] * P.inv_norm[j];
+            el = 0;
+            ret = 0.0f;
+        }
+    }
+
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = y1[j];
+        if (P.max_steps > 0 || (P.flags & RR_FLAG_EPISODE_STATS)) B.elapsed[i] = el;
+        if (P.flags & RR_FLAG_EPISODE_STATS) B.ep_ret[i] = ret;
+        io.reward[i] = r;
+        io.done[i] = (uint8_t)done;
+        if (io.truncated) io.truncated[i] = (uint8_t)trunc;
+        if (io.terms) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) io.terms[(int64_t)j * n + i] = t[j];
+            io.terms[(int64_t)NT * n + i] = bv ? 1.0f : 0.0f;           // info["bounds_violation"]
+            io.terms[(int64_t)(NT + 1) * n + i] = event ? 1.0f : 0.0f;  // solve_ivp status == 1
+        }
+    }
+    store_obs_tile<NS>(lds[wv], o, io.obs, wave_base, lane, n, io.obs_vec_ok);
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bufs B, const uint8_t* mask,
+                                                      float* obs)
+{
+    constexpr int NS = Dims<MODEL>::NS;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B.n) return;
+    const int64_t n = B.n;
+    float s[NS], v0;
+    if (mask == nullptr || mask[i]) {
+        uint4* rs = reinterpret_cast<uint4*>(B.rng) + i;
+        uint4 st = *rs;
+        Rng g{st.x, st.y, st.z, st.w};
+        sample_ic<MODEL>(P, g, s, v0);
+        *rs = make_uint4(g.s0, g.s1, g.s2, g.s3);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = s[j];
+        B.v0[i] = v0;
+        B.elapsed[i] = 0;
+        B.ep_ret[i] = 0.0f;
+    } else {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) s[j] = B.state[(int64_t)j * n + i];
+    }
+    if (obs) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) obs[i * NS + j] = s[j] * P.inv_norm[j];
+    }
+}
+
+// Compact the terminal rows of the (sorted) done list for one host copy.
+__global__ __launch_bounds__(kBlock) void gather_done_kernel(const int32_t* idx, int64_t count, int ns,
+                                                             const float* term_obs, const float* term_ret,
+                                                             const int32_t* term_len, float* g_obs, float* g_ret,
+                                                             int32_t* g_len)
+{
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= count) return;
+    const int64_t i = idx[k];
+    for (int j = 0; j < ns; ++j) g_obs[k * ns + j] = term_obs[i * ns + j];
+    g_ret[k] = term_ret[i];
+    g_len[k] = term_len[i];
+}
+
+__global__ __launch_bounds__(kBlock) void seed_kernel(uint32_t* rng, int64_t n, int64_t id_off, uint64_t seed)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint64_t x = seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(id_off + i + 1));
+    uint64_t a = splitmix64(x), b = splitmix64(x);
+    uint4 st = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    if ((st.x | st.y | st.z | st.w) == 0u) st.x = 1u;
+    reinterpret_cast<uint4*>(rng)[i] = st;
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what)
+{
+    return fail(RR_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+float ceil_f(double d)   // smallest float >= d
+{
+    float f = (float)d;
+    if ((double)f < d) f = std::nextafter(f, INFINITY);
+    return f;
+}
+float floor_f(double d)  // largest float <= d
+{
+    float f = (float)d;
+    if ((double)f > d) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+
+KParams make_kparams(const rr_params& p)
+{
+    KParams k;
+    std::memset(&k, 0, sizeof(k));
+    const int ns = p.model == RR_MODEL_6DOF ? 14 : 7;
+    k.max_steps = p.max_episode_steps;
+    k.flags = p.flags;
+    k.h = p.dt;
+    k.h2 = 0.5f * p.dt;
+    k.h6 = p.dt / 6.0f;
+    for (int j = 0; j < ns; ++j) {
+        k.ic_low[j] = p.ic_low[j];
+        k.ic_span[j] = p.ic_high[j] - p.ic_low[j];
+        k.inv_norm[j] = (float)(1.0 / (double)p.normalizer[j]);
+    }
+    for (int j = 0; j < 3; ++j) {
+        k.blo[j] = p.bounds_low[j];
+        k.bhi[j] = p.bounds_high[j];
+    }
+    k.max_gimbal = p.max_gimbal;
+    k.half_thrust = 0.5f * p.max_thrust;
+    k.alfa = p.alfa;
+    k.beta = p.beta;
+    k.eta = p.eta;
+    k.gamma = p.gamma;
+    k.delta = p.delta;
+    k.kappa = p.kappa;
+    k.xi = p.xi;
+    k.waypoint = p.waypoint;
+    k.land_r2 = (float)((double)p.landing_radius * p.landing_radius);
+    k.land_v2 = (float)((double)p.max_velocity * p.max_velocity);
+    const double pi = 3.14159265358979323846;
+    for (int ax = 0; ax < 3; ++ax) {
+        const double L = p.att_limit[ax], M = p.land_att_limit[ax];
+        if (ax == 1) {  // b = asin(R02) in [-pi/2, pi/2]
+            if (L >= pi / 2) k.att_never |= 1u << ax;
+            else k.att_c[ax] = (float)std::sin(L);
+            if (M > pi / 2) k.land_always |= 1u << ax;
+            else k.land_c[ax] = (float)std::sin(M);
+        } else {        // a, c = atan2(.) in [-pi, pi]
+            if (L >= pi) k.att_never |= 1u << ax;
+            else k.att_c[ax] = (float)std::cos(L);
+            if (M > pi) k.land_always |= 1u << ax;
+            else k.land_c[ax] = (float)std::cos(M);
+        }
+    }
+    k.omega_lt = ceil_f((double)p.omega_lim[0]);
+    k.zero_h = floor_f(1e-3);
+    k.dm = (float)(-1.0 / (9.81 * kIsp));
+    k.jinv[0] = (float)(1.0 / kJ1);
+    k.jinv[1] = (float)(1.0 / kJ2);
+    k.jinv[2] = (float)(1.0 / kJ3);
+    k.jd[0] = (float)(kJ3 - kJ2);
+    k.jd[1] = (float)(kJ1 - kJ3);
+    k.jd[2] = (float)(kJ2 - kJ1);
+    k.rt15 = (float)(-kRT);
+    k.drag3 = (float)kDrag3;
+    k.lever_over_i3 = (float)(kLever3 / kI3);
+    k.zeta_hint = (float)(pi / 2);
+    return k;
+}
+
+}  // namespace
+
+struct rr_env {
+    int device;
+    rr_params p;
+    KParams kp;
+    int ns, na, nt;
+    int64_t n, id_off;
+    uint64_t steps;
+    float* state;
+    float* v0;
+    int32_t* elapsed;
+    uint32_t* rng;
+    float* ep_ret;
+    int32_t* done_count;
+    int32_t* done_idx;
+    float* term_obs;
+    float* term_ret;
+    int32_t* term_len;
+    int32_t* g_idx;     // rr_fetch_done scratch
+    float* g_obs;
+    float* g_ret;
+    int32_t* g_len;
+};
+
+namespace {
+
+Bufs bufs_of(const rr_env* e)
+{
+    Bufs b;
+    b.state = e->state;
+    b.v0 = e->v0;
+    b.elapsed = e->elapsed;
+    b.rng = e->rng;
+    b.ep_ret = e->ep_ret;
+    b.done_count = e->done_count;
+    b.done_idx = e->done_idx;
+    b.term_obs = e->term_obs;
+    b.term_ret = e->term_ret;
+    b.term_len = e->term_len;
+    b.n = e->n;
+    b.id_off = e->id_off;
+    return b;
+}
+
+unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int rr_abi_version(void) { return RR_ABI_VERSION; }
+
+const char* rr_last_error(void) { return g_err.c_str(); }
+
+int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset, int device)
+{
+    if (!out || !p) return fail(RR_EINVAL, "rr_create: null argument");
+    *out = nullptr;
+    if (p->model != RR_MODEL_6DOF && p->model != RR_MODEL_3DOF)
+        return fail(RR_EINVAL, "rr_create: model must be 3 or 6");
+    if (p->integrator != RR_INT_RK4 && p->integrator != RR_INT_EULER)
+        return fail(RR_EINVAL, "rr_create: unknown integrator");
+    if (n <= 0 || n > (int64_t)INT32_MAX) return fail(RR_EINVAL, "rr_create: n must be in [1, 2^31)");
+    if (!(p->dt > 0.0f)) return fail(RR_EINVAL, "rr_create: dt must be > 0");
+    rr_env* e = new (std::nothrow) rr_env();
+    if (!e) return fail(RR_ENOMEM, "rr_create: host allocation failed");
+    e->device = device;
+    e->p = *p;
+    e->kp = make_kparams(*p);
+    e->ns = p->model == RR_MODEL_6DOF ? 14 : 7;
+    e->na = p->model == RR_MODEL_6DOF ? 3 : 2;
+    e->nt = p->model == RR_MODEL_6DOF ? 5 : 6;
+    e->n = n;
+    e->id_off = env_id_offset;
+    DeviceGuard g(device);
+    struct A {
+        void** ptr;
+        size_t bytes;
+    } allocs[] = {
+        {(void**)&e->state, sizeof(float) * e->ns * n},   {(void**)&e->v0, sizeof(float) * n},
+        {(void**)&e->elapsed, sizeof(int32_t) * n},       {(void**)&e->rng, sizeof(uint32_t) * 4 * n},
+        {(void**)&e->ep_ret, sizeof(float) * n},          {(void**)&e->done_count, sizeof(int32_t) * 2},
+        {(void**)&e->done_idx, sizeof(int32_t) * n},      {(void**)&e->term_obs, sizeof(float) * e->ns * n},
+        {(void**)&e->term_ret, sizeof(float) * n},        {(void**)&e->term_len, sizeof(int32_t) * n},
+        {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
+        {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
+    };
+    for (auto& a : allocs) {
+        hipError_t err = hipMalloc(a.ptr, a.bytes);
+        if (err != hipSuccess) {
+            rr_destroy(e);
+            return hip_fail(err, "rr_create: hipMalloc");
+        }
+        err = hipMemset(*a.ptr, 0, a.bytes);
+        if (err != hipSuccess) {
+            rr_destroy(e);
+            return hip_fail(err, "rr_create: hipMemset");
+        }
+    }
+    int rc = rr_seed(e, 42, nullptr);
+    if (rc == RR_OK) {
+        hipError_t err = hipDeviceSynchronize();
+        if (err != hipSuccess) rc = hip_fail(err, "rr_create: sync");
+    }
+    if (rc != RR_OK) {
+        rr_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return RR_OK;
+}
+
+int rr_destroy(rr_env* e)
+{
+    if (!e) return RR_OK;
+    DeviceGuard g(e->device);
+    void* ptrs[] = {e->state, e->v0,       e->elapsed,  e->rng,   e->ep_ret, e->done_count, e->done_idx,
+                    e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret,      e->g_len};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    delete e;
+    return RR_OK;
+}
+
+int64_t rr_num_envs(const rr_env* e) { return e ? e->n : -1; }
+int rr_state_dim(const rr_env* e) { return e ? e->ns : -1; }
+int rr_action_dim(const rr_env* e) { return e ? e->na : -1; }
+
+int rr_seed(rr_env* e, uint64_t seed, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_seed: null handle");
+    hipLaunchKernelGGL(seed_kernel, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->rng, e->n,
+                       e->id_off, seed);
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_seed: launch");
+}
+
+int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_reset: null handle");
+    const Bufs b = bufs_of(e);
+    if (e->p.model == RR_MODEL_6DOF)
+        hipLaunchKernelGGL(reset_kernel<6>, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->kp, b,
+                           mask, obs);
+    else
+        hipLaunchKernelGGL(reset_kernel<3>, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->kp, b,
+                           mask, obs);
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_reset: launch");
+}
+
+int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
+            float* terms, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_step: null handle");
+    if (!action || !obs || !reward || !done) return fail(RR_EINVAL, "rr_step: action/obs/reward/done required");
+    StepIO io;
+    io.action = action;
+    io.obs = obs;
+    io.reward = reward;
+    io.done = done;
+    io.truncated = truncated;
+    io.terms = terms;
+    io.parity = (int32_t)(e->steps & 1u);
+    io.obs_vec_ok = ((uintptr_t)obs & 15u) == 0;
+    const Bufs b = bufs_of(e);
+    const dim3 grid(grid_of(e->n)), block(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    const bool m6 = e->p.model == RR_MODEL_6DOF;
+    const bool euler = e->p.integrator == RR_INT_EULER;
+    if (m6 && !euler) hipLaunchKernelGGL((step_kernel<6, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
+    else if (m6) hipLaunchKernelGGL((step_kernel<6, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
+    else if (!euler) hipLaunchKernelGGL((step_kernel<3, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
+    else hipLaunchKernelGGL((step_kernel<3, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return hip_fail(err, "rr_step: launch");
+    e->steps++;
+    return RR_OK;
+}
+
+int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32_t* elapsed, void* stream)
+{
+    if (!e || !state_soa) return fail(RR_EINVAL, "rr_set_state: null argument");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t err = hipMemcpyAsync(e->state, state_soa, sizeof(float) * e->ns * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && v0)
+        err = hipMemcpyAsync(e->v0, v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess) {
+        if (elapsed) err = hipMemcpyAsync(e->elapsed, elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+        else err = hipMemsetAsync(e->elapsed, 0, sizeof(int32_t) * e->n, s);
+    }
+    if (err == hipSuccess) err = hipMemsetAsync(e->ep_ret, 0, sizeof(float) * e->n, s);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_set_state");
+}
+
+int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_get_state: null handle");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t err = hipSuccess;
+    if (state_soa)
+        err = hipMemcpyAsync(state_soa, e->state, sizeof(float) * e->ns * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && v0) err = hipMemcpyAsync(v0, e->v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && elapsed)
+        err = hipMemcpyAsync(elapsed, e->elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_get_state");
+}
+
+int rr_get_buffers(rr_env* e, rr_buffers* out)
+{
+    if (!e || !out) return fail(RR_EINVAL, "rr_get_buffers: null argument");
+    out->state = e->state;
+    out->v0 = e->v0;
+    out->elapsed = e->elapsed;
+    out->ep_return = e->ep_ret;
+    // the last issued step used parity (steps-1)&1
+    out->done_count = e->done_count + ((e->steps + 1) & 1u);
+    out->done_idx = e->done_idx;
+    out->terminal_obs = e->term_obs;
+    out->terminal_return = e->term_ret;
+    out->terminal_len = e->term_len;
+    return RR_OK;
+}
+
+int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs, float* term_return,
+                      int32_t* term_len, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_fetch_done: null handle");
+    if (capacity < 0) return fail(RR_EINVAL, "rr_fetch_done: negative capacity");
+    hipStream_t s = (hipStream_t)stream;
+    const int32_t* dcount = e->done_count + ((e->steps + 1) & 1u);
+    int32_t count = 0;
+    hipError_t err = hipMemcpyAsync(&count, dcount, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (err == hipSuccess) err = hipStreamSynchronize(s);
+    if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: count");
+    if (count <= 0 || e->steps == 0) return 0;
+    const int64_t m = std::min<int64_t>(count, capacity);
+    if (m == 0) return count;
+    std::vector<int32_t> hidx(count);
+    err = hipMemcpy(hidx.data(), e->done_idx, sizeof(int32_t) * count, hipMemcpyDeviceToHost);
+    if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: idx");
+    std::sort(hidx.begin(), hidx.end());
+    if (idx) std::memcpy(idx, hidx.data(), sizeof(int32_t) * m);
+    if (term_obs || term_return || term_len) {
+        err = hipMemcpyAsync(e->g_idx, hidx.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, s);
+        if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: idx upload");
+        hipLaunchKernelGGL(gather_done_kernel, dim3(grid_of(m)), dim3(kBlock), 0, s, e->g_idx, m, e->ns,
+                           e->term_obs, e->term_ret, e->term_len, e->g_obs, e->g_ret, e->g_len);
+        err = hipGetLastError();
+        if (err == hipSuccess && term_obs)
+            err = hipMemcpyAsync(term_obs, e->g_obs, sizeof(float) * e->ns * m, hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess && term_return)
+            err = hipMemcpyAsync(term_return, e->g_ret, sizeof(float) * m, hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess && term_len)
+            err = hipMemcpyAsync(term_len, e->g_len, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess) err = hipStreamSynchronize(s);
+        if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: gather");
+    }
+    return count;
+}
+
+int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* term_len, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_copy_terminal: null handle");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t err = hipSuccess;
+    if (term_obs)
+        err = hipMemcpyAsync(term_obs, e->term_obs, sizeof(float) * e->ns * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && term_return)
+        err = hipMemcpyAsync(term_return, e->term_ret, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && term_len)
+        err = hipMemcpyAsync(term_len, e->term_len, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_copy_terminal");
+}
+
+}  // extern "C"

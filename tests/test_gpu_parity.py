@@ -1,0 +1,157 @@
+"""GPU parity: the HIP step kernel (through the C-ABI) against the reference's own
+outputs (golden rows from /root/reference, tests/golden/gen_golden.py) and against
+the CPU oracle on larger seeded inputs."""
+import numpy as np
+import pytest
+
+from gpu_util import TOL_REWARD, TOL_STATE, floored_rel, run_rows
+
+pytestmark = pytest.mark.gpu
+
+ENV6 = None
+
+
+def _env6():
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    return ENV_CONFIG_6DOF
+
+
+def _check_rows(model, g, out, label):
+    ns = 14 if model == 6 else 7
+    norm = g["normalizer"][:ns]
+    e_state = floored_rel(out["state_out"], g["state_out"], norm).max(1)
+    e_obs = floored_rel(out["obs"], g["obs"], 1.0).max(1)
+    e_rew = floored_rel(out["reward"], g["reward"], 1.0)
+    e_terms = floored_rel(out["terms"], g["terms"], 1.0).max(1)
+    done_eq = out["done"] == g["done"]
+    bv_eq = out["bounds_violation"] == g["bounds_violation"]
+    ev_eq = out["event"] == (g["status"] == 1)
+    msg = "%s: max state %.3g obs %.3g reward %.3g terms %.3g; done mismatches %d, bv %d, event %d" % (
+        label, e_state.max(), e_obs.max(), e_rew.max(), e_terms.max(), (~done_eq).sum(), (~bv_eq).sum(),
+        (~ev_eq).sum())
+    print(msg)
+    bad = np.where((e_state > TOL_STATE) | (e_obs > TOL_STATE) | (e_rew > TOL_REWARD) | (e_terms > TOL_REWARD)
+                   | ~done_eq | ~bv_eq | ~ev_eq)[0]
+    for i in bad[:10]:
+        print("  row", i, "group", g["group"][i], "state_err", e_state[i], "rew", out["reward"][i], g["reward"][i],
+              "done", out["done"][i], g["done"][i], "terms", out["terms"][i], g["terms"][i])
+    assert len(bad) == 0, msg
+
+
+def test_golden6_single_step(golden6):
+    out = run_rows(6, golden6, **_env6())
+    _check_rows(6, golden6, out, "6DOF golden")
+
+
+def test_golden3_single_step(golden3):
+    out = run_rows(3, golden3)
+    _check_rows(3, golden3, out, "3DOF golden")
+
+
+@pytest.mark.parametrize("model", [6, 3])
+def test_golden_trajectories(model, golden6, golden3):
+    """G7: 50-step fixed-action trajectories chained on the GPU (fp32 state carried
+    across steps) stay within the drift envelope of the fp64 reference."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    g = golden6 if model == 6 else golden3
+    kw = _env6() if model == 6 else {}
+    ns = 14 if model == 6 else 7
+    traj = g["traj_states"]  # [k, 51, ns]
+    k = traj.shape[0]
+    b = RocketBatch(k, model=model, device="cuda:0", auto_reset=False, episode_stats=False, **kw)
+    ic = g["traj_ic"].astype(np.float32)
+    v0 = np.sqrt((ic[:, 3:6 if model == 6 else 5] ** 2).sum(1, dtype=np.float32)).astype(np.float32)
+    b.set_state(torch.from_numpy(traj[:, 0, :].astype(np.float32).T.copy()), v0=torch.from_numpy(v0))
+    act = torch.from_numpy(g["traj_actions"].astype(np.float32)).cuda()
+    worst = 0.0
+    alive = np.ones(k, bool)
+    for t in range(1, traj.shape[1]):
+        _, _, done, _ = b.step(act)
+        st = b.get_state()[0].cpu().numpy().T
+        ref = traj[:, t, :]
+        ok = alive & ~np.isnan(ref).any(1)
+        if ok.any():
+            e = floored_rel(st[ok], ref[ok], g["normalizer"][:ns]).max()
+            worst = max(worst, e)
+        alive &= ~done.cpu().numpy().astype(bool)
+    b.close()
+    print("model", model, "50-step drift", worst)
+    assert worst < 2e-4
+
+
+def _random_states6(n, seed=0):
+    """Seeded 6DOF states spanning the descent envelope (incl. near-ground rows)."""
+    rng = np.random.default_rng(seed)
+    s = np.zeros((n, 14))
+    s[:, 0] = np.where(rng.random(n) < 0.1, rng.uniform(0.01, 5, n), rng.uniform(5, 560, n))
+    s[:, 1:3] = rng.uniform(-140, 140, (n, 2))
+    s[:, 3] = rng.uniform(-80, 20, n)
+    s[:, 4:6] = rng.uniform(-20, 20, (n, 2))
+    q = rng.normal(size=(n, 4))
+    q[:, 0] += 3.0
+    s[:, 6:10] = q / np.linalg.norm(q, axis=1, keepdims=True)
+    s[:, 10:13] = rng.uniform(-0.5, 0.5, (n, 3))
+    s[:, 13] = rng.uniform(30e3, 46e3, n)
+    ic = np.tile(np.float32([500, 100, 100, -50, 0, 0, 1, 0, 0, 0, 0, 0, 0, 45e3]), (n, 1))
+    ic[:, 3:6] = rng.uniform(-55, 5, (n, 3)).astype(np.float32)
+    a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    return ic, s.astype(np.float32).astype(np.float64), a
+
+
+def test_oracle_parity_6dof_65536(oracle_mod):
+    """N = 65536 seeded rows: GPU step vs the CPU oracle (faithful scipy RK45 + event)."""
+    n = 65536
+    ic, s, a = _random_states6(n, seed=7)
+    rows = dict(group=np.zeros(n, np.int8), ic=ic, state_in=s, action=a)
+    out = run_rows(6, rows, **_env6())
+    cfg = oracle_mod.make_cfg(6, **oracle_mod.ENV_CONFIG_6DOF)
+    ref = oracle_mod.step(cfg, ic, 0.0, s, a, nthreads=8)
+    ref["event"] = ref["status"] == 1
+    g = dict(ref)
+    g["group"] = rows["group"]
+    g["normalizer"] = np.array(cfg.normalizer[:14])
+    _check_rows(6, g, out, "6DOF oracle N=65536")
+
+
+def test_full_size_properties_6dof():
+    """Size-independent properties at the benchmark size N = 524288 with auto-reset:
+    determinism, done-list == done mask, reset ICs inside init_space, unit quaternions,
+    obs == state / normalizer for non-done envs."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 524288
+    kw = _env6()
+
+    def run(steps):
+        b = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=800, **kw)
+        b.reset()
+        gen = torch.Generator(device="cuda:0")
+        gen.manual_seed(123)
+        hist = []
+        for _ in range(steps):
+            a = torch.rand((n, 3), device="cuda:0", generator=gen) * 2 - 1
+            obs, rew, done, trunc = b.step(a)
+            idx, tobs, ret, ln = b.fetch_done()
+            d = done.cpu().numpy().astype(bool)
+            assert np.array_equal(np.sort(idx), np.nonzero(d)[0])
+            hist.append((obs.clone(), rew.clone(), done.clone()))
+        st = b.get_state()[0]
+        torch.cuda.synchronize()
+        b.close()
+        return hist, st
+
+    h1, st1 = run(30)
+    h2, st2 = run(30)
+    for (o1, r1, d1), (o2, r2, d2) in zip(h1, h2):
+        assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(d1, d2)
+    assert torch.equal(st1, st2)
+    st = st1.cpu().numpy()
+    qn = np.linalg.norm(st[6:10], axis=0)
+    assert np.abs(qn - 1).max() < 1e-5
+    from rl_rocket_amd.params import config_6dof
+    cfg = config_6dof(**kw)
+    obs = h1[-1][0].cpu().numpy()
+    np.testing.assert_allclose(obs, (st.T / cfg.state_normalizer).astype(np.float32), rtol=2e-6, atol=1e-7)
