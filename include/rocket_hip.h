@@ -29,8 +29,7 @@
  *   - Every call is asynchronous on the given hipStream_t (pass as void*; NULL = the
  *     default stream). Apart from rr_fetch_done (documented as synchronising), no call
  *     synchronises, allocates or frees after rr_create, so rr_step / rr_reset can be
- *     captured into a hipGraph (capture an even number of rr_step calls: the done list
- *     is double-buffered by step parity).
+ *     captured into a hipGraph.
  *   - Return value: 0 on success, < 0 on error (RR_E*); rr_last_error() returns a
  *     thread-local message. No exception or abort crosses the ABI.
  *   - A handle is not thread-safe; use one handle per stream / GPU.
@@ -91,16 +90,14 @@ typedef struct rr_params {
     float omega_lim[3];          /* 0.2 hard-coded in the reference (rocket_env.py:656) */
 } rr_params;
 
-/* Library-owned device buffers, valid until rr_destroy. The done list refers to
- * the MOST RECENT rr_step on the handle and is overwritten by the step after next
- * (double-buffered): read it before issuing two more steps. */
+/* Library-owned device buffers, valid until rr_destroy. done_bits / terminal_* refer
+ * to the MOST RECENT rr_step on the handle (overwritten by the next step). */
 typedef struct rr_buffers {
     float* state;          /* [state_dim][N] fp32 SoA */
     float* v0;             /* [N] ||IC velocity|| of the episode (rocket_env.py:989-991) */
     int32_t* elapsed;      /* [N] TimeLimit step counter */
     float* ep_return;      /* [N] running episode return (RR_FLAG_EPISODE_STATS) */
-    int32_t* done_count;   /* [1] number of done envs in the last step */
-    int32_t* done_idx;     /* [N] their env indices (compacted by wave ballot, unordered) */
+    uint64_t* done_bits;   /* [ceil(N/64)] wave-ballot done masks: bit b of word w <=> env 64w+b done */
     float* terminal_obs;   /* [N][state_dim] final obs of env i, valid where done[i] */
     float* terminal_return;/* [N] episode return of env i, valid where done[i] */
     int32_t* terminal_len; /* [N] episode length of env i, valid where done[i] */

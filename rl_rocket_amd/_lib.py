@@ -68,8 +68,7 @@ class RrBuffers(ctypes.Structure):
         ("v0", ctypes.c_void_p),
         ("elapsed", ctypes.c_void_p),
         ("ep_return", ctypes.c_void_p),
-        ("done_count", ctypes.c_void_p),
-        ("done_idx", ctypes.c_void_p),
+        ("done_bits", ctypes.c_void_p),
         ("terminal_obs", ctypes.c_void_p),
         ("terminal_return", ctypes.c_void_p),
         ("terminal_len", ctypes.c_void_p),

@@ -83,8 +83,7 @@ struct Bufs {
     int32_t* elapsed;
     uint32_t* rng;            // [N][4] xoshiro128+ state
     float* ep_ret;
-    int32_t* done_count;      // [2]
-    int32_t* done_idx;
+    uint64_t* done_bits;      // [ceil(N/64)] wave ballot of done lanes, one word per wave
     float* term_obs;
     float* term_ret;
     int32_t* term_len;
@@ -99,7 +98,6 @@ struct StepIO {
     uint8_t* done;
     uint8_t* truncated;
     float* terms;
-    int32_t parity;
     int32_t obs_vec_ok;       // obs pointer 16-B aligned: LDS-staged float4 stores
 };
 
@@ -279,46 +277,46 @@ __device__ __forceinline__ void integrate(const KParams& P, const Ctl& c, const 
 
 // Terminal ground event (solve_ivp events=..., terminal, direction 0; scipy
 // ivp.find_active_events): sign change of the altitude between the step ends.
-// The reference returns its dense output at the brentq root; here the root of the
-// cubic Hermite interpolant of the altitude (values and exact derivatives dx/dt = v
-// at both ends) is found by safeguarded Newton, and the state is re-integrated from
-// y0 to that time.
-template <int MODEL, int INTEG>
+// The reference returns its RK45 dense output at the brentq root of the altitude
+// (ivp.py handle_events, rk.py RkDenseOutput). Here the step's dense output is the
+// cubic Hermite interpolant through (y0, f(y0)) and (y1, f(y1)) — 4th-order like the
+// reference's — its altitude root is found by safeguarded Newton, and every state
+// component is evaluated there.
+template <int MODEL>
 __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const float* y0, const float* f0,
-                                        float* y1)
+                                           float* y1)
 {
     constexpr int EV = Dims<MODEL>::EV;
     constexpr int NS = Dims<MODEL>::NS;
     const float x0 = y0[EV], x1 = y1[EV];
-    float s;
-    if (x0 == 0.0f) {
-        s = 0.0f;
-    } else if (x1 == 0.0f) {
-        return;  // root at the step end: state unchanged
-    } else {
-        const float hv0 = P.h * f0[EV];          // h * dx/dt(0)
-        const float hv1 = P.h * y1[EV + 3];      // h * dx/dt(1) = h * v_alt(1)
-        float lo = 0.0f, hi = 1.0f;              // H(lo) has the sign of x0
-        s = x0 / (x0 - x1);
+    if (x1 == 0.0f) return;  // root at the step end: state unchanged
+    float s = 0.0f;
+    float f1[NS];
+    rhs<MODEL>(P, c, y1, f1);
+    if (x0 != 0.0f) {
+        const float hv0 = P.h * f0[EV], hv1 = P.h * f1[EV];
+        float lo = 0.0f, hi = 1.0f;  // H(lo) has the sign of x0
+        s = x0 * frcp(x0 - x1);
         for (int it = 0; it < 12; ++it) {
-            float s2 = s * s, s3 = s2 * s;
-            float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
-                      (s3 - s2) * hv1;
-            float dH = (6 * s2 - 6 * s) * (x0 - x1) + (3 * s2 - 4 * s + 1) * hv0 + (3 * s2 - 2 * s) * hv1;
+            const float s2 = s * s, s3 = s2 * s;
+            const float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
+                            (s3 - s2) * hv1;
+            const float dH = (6 * s2 - 6 * s) * (x0 - x1) + (3 * s2 - 4 * s + 1) * hv0 + (3 * s2 - 2 * s) * hv1;
             if (H == 0.0f) break;
             if ((H > 0.0f) == (x0 > 0.0f)) lo = s;
             else hi = s;
-            float sn = s - H / dH;
+            float sn = s - H * frcp(dH);
             if (!(sn > lo && sn < hi)) sn = 0.5f * (lo + hi);
-            if (fabsf(sn - s) < 1e-7f) {
-                s = sn;
-                break;
-            }
+            const float ds = fabsf(sn - s);
             s = sn;
+            if (ds < 1e-7f) break;
         }
     }
-    float f_unused[NS];
-    integrate<MODEL, INTEG>(P, c, y0, s * P.h, y1, f_unused);
+    const float s2 = s * s, s3 = s2 * s;
+    const float h00 = 2 * s3 - 3 * s2 + 1, h01 = 3 * s2 - 2 * s3;
+    const float h10 = P.h * (s3 - 2 * s2 + s), h11 = P.h * (s3 - s2);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) y1[j] = h00 * y0[j] + h01 * y1[j] + h10 * f0[j] + h11 * f1[j];
 }
 
 // Sample one initial condition: gym Box.sample (uniform in [low, high], float32),
@@ -330,11 +328,12 @@ __device__ __forceinline__ void sample_ic(const KParams& P, Rng& g, float* s, fl
 #pragma unroll
     for (int j = 0; j < NS; ++j) s[j] = fmaf(P.ic_span[j], g.uniform(), P.ic_low[j]);
     if constexpr (MODEL == 6) {
-        float nq = sqrtf(s[6] * s[6] + s[7] * s[7] + s[8] * s[8] + s[9] * s[9]);
-        s[6] /= nq;
-        s[7] /= nq;
-        s[8] /= nq;
-        s[9] /= nq;
+        const float nq = sqrtf(s[6] * s[6] + s[7] * s[7] + s[8] * s[8] + s[9] * s[9]);
+        const float inq = 1.0f / nq;
+        s[6] *= inq;
+        s[7] *= inq;
+        s[8] *= inq;
+        s[9] *= inq;
         v0 = sqrtf(s[3] * s[3] + s[4] * s[4] + s[5] * s[5]);
     } else {
         v0 = sqrtf(s[3] * s[3] + s[4] * s[4]);
@@ -364,8 +363,8 @@ __device__ __forceinline__ float reward_terms(const KParams& P, const float* s, 
         }
         float nrh = sqrtf(rh0 * rh0 + rh1 * rh1 + rh2 * rh2);
         float nvh = sqrtf(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
-        float t_go = nrh / nvh;
-        float f = (-v0 / fmaxf(1e-3f, nrh)) * (-expm1f(-t_go * tau_inv));
+        float t_go = nrh * frcp(nvh);
+        float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * (-expm1f(-t_go * tau_inv));
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
         t[0] = P.alfa * sqrtf(e0 * e0 + e1 * e1 + e2 * e2);
         // thrust_penalty = beta * T (denormalised, float32)
@@ -412,8 +411,8 @@ __device__ __forceinline__ float reward_terms(const KParams& P, const float* s, 
         }
         float nrh = sqrtf(rh0 * rh0 + rh1 * rh1);
         float nvh = sqrtf(s[3] * s[3] + vh1 * vh1);
-        float t_go = nrh / nvh;
-        float f = (-v0 / fmaxf(1e-3f, nrh)) * (-expm1f(-t_go * tau_inv));
+        float t_go = nrh * frcp(nvh);
+        float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * (-expm1f(-t_go * tau_inv));
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1;
         t[0] = P.alfa * sqrtf(e0 * e0 + e1 * e1);
         t[1] = P.beta * ((a[1] + 1.0f) * P.half_thrust);
@@ -465,7 +464,6 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     const int wv = threadIdx.x / kWave;
     const int64_t n = B.n;
     const int64_t wave_base = (int64_t)blockIdx.x * kBlock + (int64_t)wv * kWave;
-    if (blockIdx.x == 0 && threadIdx.x == 0) B.done_count[io.parity ^ 1] = 0;  // next step's list
     if (wave_base >= n) return;  // wave-uniform
     const int64_t i = wave_base + lane;
     const bool valid = i < n;
@@ -487,7 +485,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
     const float g0 = y0[EV], g1 = y1[EV];
     const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
-    if (event) event_step<MODEL, INTEG>(P, c, y0, f0, y1);
+    if (event) event_step<MODEL>(P, c, y0, f0, y1);
 
     if constexpr (MODEL == 6) {
         // _normalize_quaternion (simulator.py:250)
@@ -526,16 +524,14 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
 #pragma unroll
     for (int j = 0; j < NS; ++j) o[j] = y1[j] * P.inv_norm[j];
 
-    // Done compaction: one ballot per wave, one atomic per wave with any done lane.
+    // Done compaction: one ballot per wave; lane 0 stores the wave's 64-bit done mask
+    // (every wave writes its word each step, so no clearing and no atomics; the host
+    // side expands the masks into the sorted index list, rr_fetch_done).
     const bool dv = done && valid;
     const uint64_t m = __ballot(dv);
+    if (lane == 0) B.done_bits[wave_base / kWave] = m;
     if (m) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&B.done_count[io.parity], __popcll(m));
-        base = __shfl(base, 0);
         if (dv) {
-            const int rank = __popcll(m & ((1ull << lane) - 1ull));
-            B.done_idx[base + rank] = (int32_t)i;
 #pragma unroll
             for (int j = 0; j < NS; ++j) B.term_obs[i * NS + j] = o[j];
             B.term_ret[i] = ret;
@@ -733,8 +729,7 @@ struct rr_env {
     int32_t* elapsed;
     uint32_t* rng;
     float* ep_ret;
-    int32_t* done_count;
-    int32_t* done_idx;
+    uint64_t* done_bits;
     float* term_obs;
     float* term_ret;
     int32_t* term_len;
@@ -754,8 +749,7 @@ Bufs bufs_of(const rr_env* e)
     b.elapsed = e->elapsed;
     b.rng = e->rng;
     b.ep_ret = e->ep_ret;
-    b.done_count = e->done_count;
-    b.done_idx = e->done_idx;
+    b.done_bits = e->done_bits;
     b.term_obs = e->term_obs;
     b.term_ret = e->term_ret;
     b.term_len = e->term_len;
@@ -765,6 +759,7 @@ Bufs bufs_of(const rr_env* e)
 }
 
 unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+int64_t n_words(int64_t n) { return (n + kWave - 1) / kWave; }
 
 struct DeviceGuard {
     int prev = -1;
@@ -814,8 +809,8 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     } allocs[] = {
         {(void**)&e->state, sizeof(float) * e->ns * n},   {(void**)&e->v0, sizeof(float) * n},
         {(void**)&e->elapsed, sizeof(int32_t) * n},       {(void**)&e->rng, sizeof(uint32_t) * 4 * n},
-        {(void**)&e->ep_ret, sizeof(float) * n},          {(void**)&e->done_count, sizeof(int32_t) * 2},
-        {(void**)&e->done_idx, sizeof(int32_t) * n},      {(void**)&e->term_obs, sizeof(float) * e->ns * n},
+        {(void**)&e->ep_ret, sizeof(float) * n},          {(void**)&e->done_bits, sizeof(uint64_t) * n_words(n)},
+        {(void**)&e->term_obs, sizeof(float) * e->ns * n},
         {(void**)&e->term_ret, sizeof(float) * n},        {(void**)&e->term_len, sizeof(int32_t) * n},
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
@@ -849,8 +844,8 @@ int rr_destroy(rr_env* e)
 {
     if (!e) return RR_OK;
     DeviceGuard g(e->device);
-    void* ptrs[] = {e->state, e->v0,       e->elapsed,  e->rng,   e->ep_ret, e->done_count, e->done_idx,
-                    e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret,      e->g_len};
+    void* ptrs[] = {e->state,    e->v0,       e->elapsed,  e->rng,   e->ep_ret, e->done_bits,
+                    e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     delete e;
@@ -896,7 +891,6 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
     io.done = done;
     io.truncated = truncated;
     io.terms = terms;
-    io.parity = (int32_t)(e->steps & 1u);
     io.obs_vec_ok = ((uintptr_t)obs & 15u) == 0;
     const Bufs b = bufs_of(e);
     const dim3 grid(grid_of(e->n)), block(kBlock);
@@ -948,9 +942,7 @@ int rr_get_buffers(rr_env* e, rr_buffers* out)
     out->v0 = e->v0;
     out->elapsed = e->elapsed;
     out->ep_return = e->ep_ret;
-    // the last issued step used parity (steps-1)&1
-    out->done_count = e->done_count + ((e->steps + 1) & 1u);
-    out->done_idx = e->done_idx;
+    out->done_bits = e->done_bits;
     out->terminal_obs = e->term_obs;
     out->terminal_return = e->term_ret;
     out->terminal_len = e->term_len;
@@ -962,19 +954,25 @@ int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs
 {
     if (!e) return fail(RR_EINVAL, "rr_fetch_done: null handle");
     if (capacity < 0) return fail(RR_EINVAL, "rr_fetch_done: negative capacity");
+    if (e->steps == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    const int32_t* dcount = e->done_count + ((e->steps + 1) & 1u);
-    int32_t count = 0;
-    hipError_t err = hipMemcpyAsync(&count, dcount, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    const int64_t nw = n_words(e->n);
+    std::vector<uint64_t> bits(nw);
+    hipError_t err = hipMemcpyAsync(bits.data(), e->done_bits, sizeof(uint64_t) * nw, hipMemcpyDeviceToHost, s);
     if (err == hipSuccess) err = hipStreamSynchronize(s);
-    if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: count");
-    if (count <= 0 || e->steps == 0) return 0;
+    if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: done bits");
+    std::vector<int32_t> hidx;
+    for (int64_t w = 0; w < nw; ++w) {
+        uint64_t m = bits[w];
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            hidx.push_back((int32_t)(w * kWave + b));
+            m &= m - 1;
+        }
+    }
+    const int64_t count = (int64_t)hidx.size();
     const int64_t m = std::min<int64_t>(count, capacity);
     if (m == 0) return count;
-    std::vector<int32_t> hidx(count);
-    err = hipMemcpy(hidx.data(), e->done_idx, sizeof(int32_t) * count, hipMemcpyDeviceToHost);
-    if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: idx");
-    std::sort(hidx.begin(), hidx.end());
     if (idx) std::memcpy(idx, hidx.data(), sizeof(int32_t) * m);
     if (term_obs || term_return || term_len) {
         err = hipMemcpyAsync(e->g_idx, hidx.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, s);

@@ -1,0 +1,211 @@
+"""``RocketVecEnv``: a stable-baselines3 ``VecEnv`` over N GPU-resident rocket envs.
+
+Equivalent, for SB3's PPO, to ``DummyVecEnv([make_env] * N)`` with
+``make_env`` = ``gym.make(id, **env_config)`` -> ``TimeLimit(max_episode_steps)``
+-> ``Monitor`` (reference main_6DOF.py:64-70), but stepped by ONE launch of the
+fused HIP kernel for all N envs:
+
+  * on-device auto-reset; ``infos[i]["terminal_observation"]`` holds the final
+    observation of a done env and ``infos[i]["TimeLimit.truncated"]`` is set on
+    time-outs, exactly as SB3 1.6 DummyVecEnv + gym 0.21 TimeLimit do;
+  * Monitor episode statistics ``infos[i]["episode"] = {"r", "l", "t"}`` for done envs;
+  * ``infos`` is a lazy sequence: dicts are only materialised for done envs (and
+    ``rewards_dict`` / ``bounds_violation`` only when ``info_terms=True``), so the
+    host cost per step is O(#done), not O(N) dict building.
+
+``device_outputs=True`` returns torch tensors that stay in HBM (no host copy);
+otherwise numpy arrays as SB3 expects.
+"""
+import time
+from collections.abc import Sequence
+
+import numpy as np
+
+from .batch import RocketBatch
+from .gym_compat import Box
+from .params import MAX_EPISODE_STEPS, parse_model
+
+try:  # pragma: no cover - SB3 is optional (absent from this image)
+    from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _VecEnvBase
+except Exception:  # pragma: no cover
+    _VecEnvBase = object
+
+
+class LazyInfos(Sequence):
+    """SB3 ``infos`` list whose dicts are built on access."""
+
+    def __init__(self, n, done_info, terms=None, term_names=None, extra=None):
+        self._n = n
+        self._done = done_info          # {env_idx: dict}
+        self._terms = terms             # host [n_terms+2, N] array or None
+        self._names = term_names
+        self._extra = extra or {}
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(self._n))]
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError(i)
+        d = self._done.get(i)
+        if d is None:
+            d = {}
+            if self._terms is not None:
+                self._fill_terms(i, d)
+                self._done[i] = d
+        return d
+
+    def _fill_terms(self, i, d):
+        t = self._terms
+        d["rewards_dict"] = {k: float(t[j, i]) for j, k in enumerate(self._names)}
+        d["bounds_violation"] = bool(t[len(self._names), i] > 0.5)
+
+    def done_indices(self):
+        return sorted(k for k, v in self._done.items() if "terminal_observation" in v)
+
+
+class RocketVecEnv(_VecEnvBase):
+    metadata = {"render.modes": []}
+
+    def __init__(self, num_envs, model="6DOF", device=None, max_episode_steps=MAX_EPISODE_STEPS, monitor=True,
+                 reward_annealing=False, integrator="rk4", info_terms=False, device_outputs=False,
+                 env_id_offset=0, seed=None, **env_kwargs):
+        self.model = parse_model(model)
+        self.batch = RocketBatch(num_envs, model=self.model, device=device, max_episode_steps=max_episode_steps,
+                                 auto_reset=True, episode_stats=monitor, reward_annealing=reward_annealing,
+                                 integrator=integrator, env_id_offset=env_id_offset, compute_terms=info_terms,
+                                 seed=seed, **env_kwargs)
+        ns, na = self.batch.state_dim, self.batch.action_dim
+        self.num_envs = int(num_envs)
+        self.observation_space = Box(low=-1, high=1, shape=(ns,)).to_gym()
+        self.action_space = Box(low=-1, high=1, shape=(na,)).to_gym()
+        self.monitor = monitor
+        self.info_terms = info_terms
+        self.device_outputs = device_outputs
+        self.max_episode_steps = max_episode_steps
+        self._actions = None
+        self._t_start = time.time()
+        self.episode_returns = []
+        self.episode_lengths = []
+        self.episode_times = []
+        self.total_steps = 0
+        self.cfg = self.batch.cfg
+        self.state_names = self.batch.cfg.state_names if hasattr(self.batch.cfg, "state_names") else None
+
+    # -- VecEnv API ------------------------------------------------------------------------------------------
+    def reset(self):
+        obs = self.batch.reset()
+        return obs if self.device_outputs else obs.cpu().numpy()
+
+    def step_async(self, actions):
+        self._actions = actions
+
+    def step_wait(self):
+        obs, rew, done, trunc = self.batch.step(self._actions)
+        self.total_steps += self.num_envs
+        if self.device_outputs:
+            return obs, rew, done.bool(), self._lazy_infos_device(done, trunc)
+        obs_h = obs.cpu().numpy()
+        rew_h = rew.cpu().numpy()
+        done_h = done.cpu().numpy().astype(bool)
+        infos = self._infos_from_host(done_h, trunc)
+        return obs_h, rew_h, done_h, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def _infos_from_host(self, done_h, trunc):
+        done_info = {}
+        if done_h.any():
+            idx, tobs, ret, ln = self.batch.fetch_done()
+            trunc_h = trunc.cpu().numpy()
+            now = round(time.time() - self._t_start, 6)
+            for k, i in enumerate(idx.tolist()):
+                d = {"terminal_observation": tobs[k].copy()}
+                if trunc_h[i]:
+                    d["TimeLimit.truncated"] = True
+                elif self.max_episode_steps and ln[k] >= self.max_episode_steps:
+                    d["TimeLimit.truncated"] = False
+                if self.monitor:
+                    d["episode"] = {"r": round(float(ret[k]), 6), "l": int(ln[k]), "t": now}
+                    self.episode_returns.append(float(ret[k]))
+                    self.episode_lengths.append(int(ln[k]))
+                    self.episode_times.append(now)
+                done_info[i] = d
+        terms = self.batch.terms.cpu().numpy() if self.info_terms else None
+        if terms is not None:
+            for i, d in done_info.items():
+                LazyInfos._fill_terms(LazyInfos(0, {}, terms, self.cfg.term_names), i, d)
+        return LazyInfos(self.num_envs, done_info, terms, self.cfg.term_names)
+
+    def _lazy_infos_device(self, done, trunc):
+        batch = self
+
+        class _DeviceInfos(LazyInfos):
+            def __init__(self):
+                super().__init__(batch.num_envs, None)
+                self._built = None
+
+            def _build(self):
+                if self._built is None:
+                    self._built = batch._infos_from_host(done.cpu().numpy().astype(bool), trunc)
+                return self._built
+
+            def __getitem__(self, i):
+                return self._build()[i]
+
+            def done_indices(self):
+                return self._build().done_indices()
+
+        return _DeviceInfos()
+
+    def close(self):
+        self.batch.close()
+
+    def seed(self, seed=None):
+        if seed is None:
+            seed = int(np.random.randint(0, 2 ** 31 - 1))
+        self.batch.seed(seed)
+        return [seed + i for i in range(self.num_envs)]
+
+    def _indices(self, indices):
+        if indices is None:
+            return range(self.num_envs)
+        if isinstance(indices, int):
+            return [indices]
+        return indices
+
+    def get_attr(self, attr_name, indices=None):
+        value = getattr(self, attr_name, None)
+        if value is None:
+            value = getattr(self.batch.cfg, attr_name, None)
+        if value is None and attr_name in self.batch.cfg.kwargs:
+            value = self.batch.cfg.kwargs[attr_name]
+        if value is None and attr_name == "reward_coefficients":
+            value = self.batch.cfg.kwargs["reward_coeff"]
+        return [value for _ in self._indices(indices)]
+
+    def set_attr(self, attr_name, value, indices=None):
+        raise AttributeError("RocketVecEnv envs share one device-resident config; %r cannot be set per env"
+                             % attr_name)
+
+    def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+        raise AttributeError("RocketVecEnv has no per-env python objects (method %r)" % method_name)
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False for _ in self._indices(indices)]
+
+    def render(self, mode="human"):
+        return None
+
+    def get_images(self):
+        return []
+
+    @property
+    def unwrapped(self):
+        return self

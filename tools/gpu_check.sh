@@ -25,4 +25,10 @@ cd /tmp || exit 2
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python "$R/bench.py" --no-cpu-baseline > "$OUT/prof_bench.log" 2>&1
 ok_or_testfail $? rocprof
 find "$OUT/prof" -name '*stats*' | head
+if [ -n "$PMC" ]; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $PMC_ARGS > "$OUT/pmc_$C.log" 2>&1
+    ok_or_testfail $? pmc_$C
+  done
+fi
 echo done
