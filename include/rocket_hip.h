@@ -95,7 +95,7 @@ typedef struct rr_params {
 typedef struct rr_buffers {
     float* state;          /* [state_dim][N] fp32 SoA */
     float* v0;             /* [N] ||IC velocity|| of the episode (rocket_env.py:989-991) */
-    int32_t* elapsed;      /* [N] TimeLimit step counter */
+    int32_t* elapsed;      /* [N] counter word: TimeLimit steps (bits 0-15) | episode (bits 16-31) */
     float* ep_return;      /* [N] running episode return (RR_FLAG_EPISODE_STATS) */
     uint64_t* done_bits;   /* [ceil(N/64)] wave-ballot done masks: bit b of word w <=> env 64w+b done */
     float* terminal_obs;   /* [N][state_dim] final obs of env i, valid where done[i] */
@@ -117,7 +117,10 @@ int64_t rr_num_envs(const rr_env* e);
 int rr_state_dim(const rr_env* e);
 int rr_action_dim(const rr_env* e);
 
-/* Re-seed every env's reset stream: seed + global env id (counter-free, deterministic). */
+/* Set the key of the reset stream. Resets are counter-based: env `gid` starting its
+ * episode `e` draws its initial condition from splitmix64/xoshiro128+ keyed on
+ * (seed, gid, e, bits of the state it replaces) — deterministic, independent of how
+ * envs are sharded over GPUs, and free of per-env RNG state in HBM. Host-only call. */
 int rr_seed(rr_env* e, uint64_t seed, void* stream);
 /* Sample a fresh initial condition for every env where mask[i] != 0 (all when mask is
  * NULL), write the normalised obs [N][state_dim] (obs may be NULL). */
@@ -137,8 +140,9 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
             float* terms, void* stream);
 
 /* Overwrite / read the per-env state (parity injection, checkpoint / restore).
- * state_soa [state_dim][N] fp32; v0 [N] or NULL (then recomputed from nothing: kept);
- * elapsed [N] or NULL (then zeroed on set / skipped on get). */
+ * state_soa [state_dim][N] fp32; v0 [N] or NULL (kept on set / skipped on get);
+ * elapsed [N] or NULL (zeroed on set / skipped on get) is the per-env counter word:
+ * TimeLimit steps in bits 0-15, episodes started in bits 16-31 (keys the reset stream). */
 int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32_t* elapsed, void* stream);
 int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void* stream);
 

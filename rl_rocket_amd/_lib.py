@@ -10,7 +10,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librocket_hip.so")
+LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
 ABI_VERSION = 1

@@ -22,9 +22,11 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def command(resource_usage=False):
-    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT, SRC]
+def command(resource_usage=False, out=OUT, defines=()):
+    # -fno-slp-vectorize: the SLP pass packs scalar f32 math into v_pk_* pairs and adds ~180
+    # register moves to the step kernel (measured on the .s); the scalar stream is shorter.
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-fno-slp-vectorize", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(ROOT, "include")] + ["-D%s" % d for d in defines] + ["-o", out, SRC]
     if resource_usage:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     return cmd

@@ -28,6 +28,13 @@
 
 #include "rocket_hip.h"
 
+// Diagnostic ablations (tools/diag_kernel.py only; the product build has RR_DIAG 0):
+//   1 = memory only (no integration / reward arithmetic), 2 = no event / reset branches,
+//   3 = compute only (state synthesised in registers instead of loaded).
+#ifndef RR_DIAG
+#define RR_DIAG 0
+#endif
+
 namespace {
 
 constexpr int kWave = 64;
@@ -48,6 +55,21 @@ constexpr double kRT = -15.0;
 constexpr double kDrag3 = 0.5 * 1.225 * 0.3 * 10.5;  // A = Cd * (0.5 rho v^2) * Sref
 constexpr double kLever3 = 40.0 - 10.0;               // x_T - x_CG
 constexpr double kI3 = 6.04e6;
+// folded into the device code as immediates
+constexpr float kDmScale = (float)(-1.0 / (9.81 * kIsp));  // dm = T * kDmScale
+constexpr float kJinv2 = (float)(1.0 / kJ2), kJinv3 = (float)(1.0 / kJ3);
+constexpr float kJd1 = (float)(kJ1 - kJ3), kJd2 = (float)(kJ2 - kJ1);  // (w x Jw)_1 = kJd1 w1 w3, _2 = kJd2 w1 w2
+constexpr float kRt = (float)(-kRT);  // tau = r_T_B x T_b = [0, 15 Tbz, -15 Tby]
+static_assert(kJ2 == kJ3, "omega_1 is constant only for an axisymmetric body (J2 == J3)");
+constexpr float kDrag3f = (float)kDrag3;
+constexpr float kLeverOverI3 = (float)(kLever3 / kI3);
+constexpr float kHalfPi = 1.57079632679489662f;
+constexpr float kTwoPi = 6.28318530717958648f;
+
+// Per-env counter word: TimeLimit steps in the low 16 bits, episodes started in the
+// high 16 bits (keys the counter-based reset stream).
+constexpr uint32_t kElapsedMask = 0xFFFFu;
+constexpr int kEpisodeShift = 16;
 
 // Device-side constants, derived once on the host from rr_params (see make_kparams).
 struct KParams {
@@ -69,26 +91,20 @@ struct KParams {
     uint32_t land_always;     // bit k: "|e_k| < limit" always holds
     float omega_lt;           // |w| < omega_lim  (float threshold, reference 0.2)
     float zero_h;             // x <= 1e-3 as a float threshold
-    float dm;                 // -1/(g0*Isp) scale: dm = T * dm
-    // 6DOF rotational constants
-    float jinv[3], jd[3];     // 1/J_i and (J3-J2, J1-J3, J2-J1)
-    float rt15;               // -r_T_B x  -> tau = [0, 15 Tbz, -15 Tby]
-    // 3DOF
-    float drag3, lever_over_i3, zeta_hint;  // zeta_hint = pi/2
+    uint64_t seed;            // reset stream key (rr_seed)
+    int64_t id_off;           // global id of env 0 (multi-GPU shards)
 };
 
 struct Bufs {
     float* state;
     float* v0;
-    int32_t* elapsed;
-    uint32_t* rng;            // [N][4] xoshiro128+ state
+    uint32_t* counter;        // [N] elapsed | episode << 16
     float* ep_ret;
     uint64_t* done_bits;      // [ceil(N/64)] wave ballot of done lanes, one word per wave
     float* term_obs;
     float* term_ret;
     int32_t* term_len;
     int64_t n;
-    int64_t id_off;
 };
 
 struct StepIO {
@@ -102,10 +118,57 @@ struct StepIO {
 };
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// Raw buffer access (SRSRC descriptor built from wave-uniform values): 32-bit per-lane
+// voffset, per-plane offsets in soffset (SGPR) — no per-lane 64-bit address arithmetic.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint64_t bytes)
+{
+    const uint32_t nr = bytes >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)nr, 0x00020000);
+}
+__device__ __forceinline__ float bld_f(rsrc_t r, uint32_t voff, uint32_t soff)
+{
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ uint32_t bld_u(rsrc_t r, uint32_t voff, uint32_t soff)
+{
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void bst_f(rsrc_t r, float v, uint32_t voff, uint32_t soff)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void bst_u(rsrc_t r, uint32_t v, uint32_t voff, uint32_t soff)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void bst_u8(rsrc_t r, uint8_t v, uint32_t voff)
+{
+    __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)voff, 0, 0);
+}
+
+// Element idx of a wave-uniform base pointer with a 32-bit byte offset: lowers to the
+// saddr + voffset form of global_load/store (no per-lane 64-bit address arithmetic).
+template <class T>
+__device__ __forceinline__ T& at(T* base, uint32_t idx)
+{
+    return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (uint32_t)(idx * (uint32_t)sizeof(T)));
+}
+template <class T>
+__device__ __forceinline__ const T& at(const T* base, uint32_t idx)
+{
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (uint32_t)(idx * (uint32_t)sizeof(T)));
+}
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
 
 // ---------------------------------------------------------------------------
-// xoshiro128+ per-env reset stream (16 B of state, touched only on reset).
+// Reset stream: counter-based. A reset of env `gid` in its episode `ep` seeds a
+// register-resident xoshiro128+ from splitmix64(seed, gid, ep, bits of the state being
+// replaced); no per-env RNG state lives in HBM and no memory access is needed.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 
@@ -131,6 +194,16 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t& x)
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ Rng reset_rng(uint64_t seed, int64_t gid, uint32_t episode, float salt_a, float salt_b)
+{
+    uint64_t x = seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(gid + 1));
+    x ^= (uint64_t)episode * 0xA0761D6478BD642Full;
+    x ^= ((uint64_t)__float_as_uint(salt_a) << 32) | (uint64_t)__float_as_uint(salt_b);
+    const uint64_t a = splitmix64(x), b = splitmix64(x);
+    Rng g{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32) | 1u};
+    return g;
 }
 
 // ---------------------------------------------------------------------------
@@ -168,59 +241,61 @@ __device__ __forceinline__ Ctl make_ctl(const KParams& P, const float* a)
         c.tbx = T * (cy * cz);
         c.tby = T * (sy * cz);
         c.tbz = T * sz;
-        c.tau1 = P.rt15 * c.tbz;
-        c.tau2 = -P.rt15 * c.tby;
-        c.dm = T * P.dm;
+        c.tau1 = (kRt * kJinv2) * c.tbz;   // J2^-1 tau_1
+        c.tau2 = (-kRt * kJinv3) * c.tby;  // J3^-1 tau_2
+        c.dm = T * kDmScale;
     } else {
         float d = a[0] * P.max_gimbal;
         float T = (a[1] + 1.0f) * P.half_thrust;
         c.sd = __sinf(d);
         c.cd = __cosf(d);
         c.thrust = T;
-        c.dom = -(T * c.sd) * P.lever_over_i3;
-        c.dm = T * P.dm;
+        c.dom = -(T * c.sd) * kLeverOverI3;
+        c.dm = T * kDmScale;
     }
     return c;
 }
 
-// 6DOF RHS, simulator.py:259-294. R(q/|q|) T_b is applied as a quaternion rotation
-// (t = 2 u x T_b; F = T_b + w t + u x t) — the same rotation as scipy's as_matrix().
+// 6DOF RHS, simulator.py:259-294. R(q/|q|) T_b (scipy Rotation.from_quat normalises,
+// simulator.py:346) is applied as a quaternion rotation of the UNnormalised q scaled by
+// 1/|q|^2 (R is homogeneous of degree 2 in q):  |q|^2 R T_b = |q|^2 T_b + w t + u x t,
+// t = 2 u x T_b; the division by |q|^2 folds into the division by the mass.
 template <int MODEL>
 __device__ __forceinline__ void rhs(const KParams& P, const Ctl& c, const float* s, float* d)
 {
     if constexpr (MODEL == 6) {
         const float q0 = s[6], q1 = s[7], q2 = s[8], q3 = s[9];
         const float w1 = s[10], w2 = s[11], w3 = s[12];
-        float rn = frsq(q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3);
-        float w = q0 * rn, ux = q1 * rn, uy = q2 * rn, uz = q3 * rn;
-        float tx = 2.0f * (uy * c.tbz - uz * c.tby);
-        float ty = 2.0f * (uz * c.tbx - ux * c.tbz);
-        float tz = 2.0f * (ux * c.tby - uy * c.tbx);
-        float Fx = c.tbx + w * tx + (uy * tz - uz * ty);
-        float Fy = c.tby + w * ty + (uz * tx - ux * tz);
-        float Fz = c.tbz + w * tz + (ux * ty - uy * tx);
-        float im = frcp(s[13]);
+        const float qq = q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;
+        const float tx = 2.0f * (q2 * c.tbz - q3 * c.tby);
+        const float ty = 2.0f * (q3 * c.tbx - q1 * c.tbz);
+        const float tz = 2.0f * (q1 * c.tby - q2 * c.tbx);
+        const float Fx = qq * c.tbx + q0 * tx + (q2 * tz - q3 * ty);
+        const float Fy = qq * c.tby + q0 * ty + (q3 * tx - q1 * tz);
+        const float Fz = qq * c.tbz + q0 * tz + (q1 * ty - q2 * tx);
+        const float sc = frcp(qq * s[13]);
         d[0] = s[3];
         d[1] = s[4];
         d[2] = s[5];
-        d[3] = Fx * im - kG0;
-        d[4] = Fy * im;
-        d[5] = Fz * im;
+        d[3] = Fx * sc - kG0;
+        d[4] = Fy * sc;
+        d[5] = Fz * sc;
         // dq = 0.5 Omega(w) q with the unnormalised q (simulator.py:287, :362-370)
-        d[6] = 0.5f * (-w1 * q1 - w2 * q2 - w3 * q3);
-        d[7] = 0.5f * (w1 * q0 + w3 * q2 - w2 * q3);
-        d[8] = 0.5f * (w2 * q0 - w3 * q1 + w1 * q3);
-        d[9] = 0.5f * (w3 * q0 + w2 * q1 - w1 * q2);
-        // dw = J^-1 (tau - w x Jw) (simulator.py:288)
-        d[10] = P.jinv[0] * (-(P.jd[0] * (w2 * w3)));
-        d[11] = P.jinv[1] * (c.tau1 - P.jd[1] * (w1 * w3));
-        d[12] = P.jinv[2] * (c.tau2 - P.jd[2] * (w1 * w2));
+        const float h1 = 0.5f * w1, h2 = 0.5f * w2, h3 = 0.5f * w3;
+        d[6] = -h1 * q1 - h2 * q2 - h3 * q3;
+        d[7] = h1 * q0 + h3 * q2 - h2 * q3;
+        d[8] = h2 * q0 - h3 * q1 + h1 * q3;
+        d[9] = h3 * q0 + h2 * q1 - h1 * q2;
+        // dw = J^-1 (tau - w x Jw) (simulator.py:288); J2 == J3 makes dw_1 = 0
+        d[10] = 0.0f;
+        d[11] = c.tau1 - (kJd1 * kJinv2) * (w1 * w3);
+        d[12] = c.tau2 - (kJd2 * kJinv3) * (w1 * w2);
         d[13] = c.dm;
     } else {
         // 3DOF RHS, simulator.py:88-130 (N = 0; the z-drag uses cos(phi): reference quirk)
         const float th = s[2], vx = s[3], vz = s[4];
         float st = __sinf(th), ct = __cosf(th);
-        float A = P.drag3 * (vx * vx + vz * vz);
+        float A = kDrag3f * (vx * vx + vz * vz);
         float cdt = c.cd * ct - c.sd * st;   // cos(delta + phi)
         float sdt = c.sd * ct + c.cd * st;   // sin(delta + phi)
         float im = frcp(s[6]);
@@ -417,9 +492,9 @@ __device__ __forceinline__ float reward_terms(const KParams& P, const float* s, 
         t[0] = P.alfa * sqrtf(e0 * e0 + e1 * e1);
         t[1] = P.beta * ((a[1] + 1.0f) * P.half_thrust);
         t[2] = P.eta;
-        float zeta = fabsf(s[2] - P.zeta_hint);
-        t[3] = zeta > 2.0f * 3.14159265358979f ? P.gamma : 0.0f;
-        t[4] = P.delta * fmaxf(0.0f, zeta - P.zeta_hint);
+        float zeta = fabsf(s[2] - kHalfPi);
+        t[3] = zeta > kTwoPi ? P.gamma : 0.0f;
+        t[4] = P.delta * fmaxf(0.0f, zeta - kHalfPi);
         // _check_landing (rocket_env.py:449-476)
         float r2 = s[0] * s[0] + s[1] * s[1];
         float v2 = s[3] * s[3] + s[4] * s[4];
@@ -433,59 +508,99 @@ __device__ __forceinline__ float reward_terms(const KParams& P, const float* s, 
 
 // Write this wave's [64][NS] observation tile through LDS as 16-B coalesced stores.
 template <int NS>
-__device__ __forceinline__ void store_obs_tile(float* lds, const float* o, float* obs, int64_t wave_base,
-                                               int lane, int64_t n, bool vec_ok)
+__device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_t obs_r, uint32_t wave_base,
+                                               int lane, uint32_t nvalid, bool vec_ok)
 {
+    if constexpr (NS % 2 == 0) {
+        float2* l2 = reinterpret_cast<float2*>(lds + lane * NS);
 #pragma unroll
-    for (int j = 0; j < NS; ++j) lds[lane * NS + j] = o[j];
+        for (int j = 0; j < NS / 2; ++j) l2[j] = make_float2(o[2 * j], o[2 * j + 1]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) lds[lane * NS + j] = o[j];
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int64_t nvalid = (n - wave_base) < kWave ? (n - wave_base) : kWave;
-    float* dst = obs + wave_base * NS;
+    const uint32_t sbase = wave_base * NS * 4u;  // byte offset of the tile (wave-uniform)
     if (vec_ok && nvalid == kWave) {
         constexpr int NV = kWave * NS / 4;
-        const float4* src4 = reinterpret_cast<const float4*>(lds);
-        float4* dst4 = reinterpret_cast<float4*>(dst);
+        const u32x4* src4 = reinterpret_cast<const u32x4*>(lds);
 #pragma unroll
-        for (int k = lane; k < NV; k += kWave) dst4[k] = src4[k];
+        for (int k = lane; k < NV; k += kWave)
+            __builtin_amdgcn_raw_buffer_store_b128(src4[k], obs_r, (int)(k * 16u), (int)sbase, 0);
     } else {
         const int tot = (int)nvalid * NS;
-        for (int k = lane; k < tot; k += kWave) dst[k] = lds[k];
+        for (int k = lane; k < tot; k += kWave) bst_f(obs_r, lds[k], k * 4u, sbase);
     }
 }
 
+// One launch = one env step of all N envs. Every HBM access goes through a buffer
+// descriptor: the per-lane byte offset is one 32-bit VGPR (i*4), plane offsets are
+// wave-uniform soffsets (NS*N*4 < 4 GiB, checked at rr_create).
 template <int MODEL, int INTEG>
 __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Bufs B, const StepIO io)
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][kWave * NS];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    const int64_t n = B.n;
-    const int64_t wave_base = (int64_t)blockIdx.x * kBlock + (int64_t)wv * kWave;
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wv = threadIdx.x / kWave;
+    const uint32_t n = (uint32_t)B.n;
+    const uint32_t wave_base = blockIdx.x * kBlock + wv * kWave;
     if (wave_base >= n) return;  // wave-uniform
-    const int64_t i = wave_base + lane;
+    const uint32_t i = wave_base + lane;
     const bool valid = i < n;
-    const int64_t ic = valid ? i : n - 1;
+    const uint32_t ic = valid ? i : n - 1;
+    const uint32_t vo = ic * 4u;           // per-lane byte offset in every fp32/u32 plane
+    const uint32_t plane = n * 4u;         // bytes per plane
+    const bool use_counter = P.max_steps > 0 || (P.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
+    const rsrc_t st_r = make_rsrc(B.state, (uint64_t)NS * plane);
+    const rsrc_t act_r = make_rsrc(io.action, (uint64_t)NA * plane);
+    const rsrc_t v0_r = make_rsrc(B.v0, plane);
+    const rsrc_t cw_r = make_rsrc(B.counter, plane);
+    const rsrc_t ret_r = make_rsrc(B.ep_ret, plane);
 
+    // ---- all loads first (one memory round trip per wave) ----
     float y0[NS], y1[NS], f0[NS], a[NA];
+#if RR_DIAG == 3
 #pragma unroll
-    for (int j = 0; j < NS; ++j) y0[j] = B.state[(int64_t)j * n + ic];
+    for (int j = 0; j < NS; ++j) y0[j] = P.ic_low[j] + P.ic_span[j] * (float)(lane & 15) * (1.0f / 16.0f);
+#else
+#pragma unroll
+    for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
+#endif
     if (P.flags & RR_FLAG_ACTION_SOA) {
 #pragma unroll
-        for (int j = 0; j < NA; ++j) a[j] = io.action[(int64_t)j * n + ic];
+        for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
+    } else if constexpr (NA == 3) {
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)(ic * 12u), 0, 0);
+        a[0] = __uint_as_float(v.x);
+        a[1] = __uint_as_float(v.y);
+        a[2] = __uint_as_float(v.z);
     } else {
-#pragma unroll
-        for (int j = 0; j < NA; ++j) a[j] = io.action[ic * NA + j];
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(ic * 8u), 0, 0);
+        a[0] = __uint_as_float(v.x);
+        a[1] = __uint_as_float(v.y);
     }
-    float v0 = B.v0[ic];
+    float v0 = bld_f(v0_r, vo, 0);
+    uint32_t cw = use_counter ? bld_u(cw_r, vo, 0) : 0u;
+    float ret = (P.flags & RR_FLAG_EPISODE_STATS) ? bld_f(ret_r, vo, 0) : 0.0f;
 
+#if RR_DIAG == 1
+#pragma unroll
+    for (int j = 0; j < NS; ++j) y1[j] = y0[j] + 1e-7f * a[j % NA];
+    const bool event = false;
+#else
     const Ctl c = make_ctl<MODEL>(P, a);
     integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
     const float g0 = y0[EV], g1 = y1[EV];
+#if RR_DIAG == 2
+    const bool event = false;
+#else
     const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
+#endif
     if (event) event_step<MODEL>(P, c, y0, f0, y1);
+#endif
 
     if constexpr (MODEL == 6) {
         // _normalize_quaternion (simulator.py:250)
@@ -496,29 +611,35 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
         y1[9] *= rn;
     } else {
         // _wrapTo2Pi (simulator.py:150-163): fmod(fmod(theta, 2pi) + 2pi, 2pi)
-        const float two_pi = 6.28318530717958647692f;
-        float th = fmodf(y1[2], two_pi) + two_pi;
-        y1[2] = fmodf(th, two_pi);
+        float th = fmodf(y1[2], kTwoPi) + kTwoPi;
+        y1[2] = fmodf(th, kTwoPi);
     }
 
     bool bv;
     float t[NT];
+#if RR_DIAG == 1
+    bv = y1[0] > 1e30f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) t[j] = 0.0f;
+    float r = v0;
+#else
     float r = reward_terms<MODEL>(P, y1, a, v0, bv, t);
+#endif
+#if RR_DIAG == 2
+    bool done = false;
+#else
     bool done = event || bv;
+#endif
 
     // gym TimeLimit (main_6DOF.py:67): elapsed += 1; at the limit done = True and
     // info["TimeLimit.truncated"] = not done
     bool trunc = false;
-    int32_t el = 0;
-    if (P.max_steps > 0 || (P.flags & RR_FLAG_EPISODE_STATS)) {
-        el = B.elapsed[ic] + 1;
-        if (P.max_steps > 0 && el >= P.max_steps) {
-            trunc = !done;
-            done = true;
-        }
+    int32_t el = (int32_t)(cw & kElapsedMask) + 1;
+    if (P.max_steps > 0 && el >= P.max_steps) {
+        trunc = !done;
+        done = true;
     }
-    float ret = 0.0f;
-    if (P.flags & RR_FLAG_EPISODE_STATS) ret = B.ep_ret[ic] + r;
+    ret += r;
 
     float o[NS];
 #pragma unroll
@@ -532,41 +653,45 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     if (lane == 0) B.done_bits[wave_base / kWave] = m;
     if (m) {
         if (dv) {
+            float* to = B.term_obs + (size_t)i * NS;
 #pragma unroll
-            for (int j = 0; j < NS; ++j) B.term_obs[i * NS + j] = o[j];
+            for (int j = 0; j < NS; ++j) to[j] = o[j];
             B.term_ret[i] = ret;
             B.term_len[i] = el;
         }
         if ((P.flags & RR_FLAG_AUTO_RESET) && dv) {
-            uint4* rs = reinterpret_cast<uint4*>(B.rng) + i;
-            uint4 st = *rs;
-            Rng g{st.x, st.y, st.z, st.w};
+            const uint32_t ep = (cw >> kEpisodeShift) + 1u;
+            Rng g = reset_rng(P.seed, P.id_off + i, ep, y1[0], y1[NS - 1]);
             sample_ic<MODEL>(P, g, y1, v0);
-            *rs = make_uint4(g.s0, g.s1, g.s2, g.s3);
             B.v0[i] = v0;
+            cw = ep << kEpisodeShift;
 #pragma unroll
             for (int j = 0; j < NS; ++j) o[j] = y1[j] * P.inv_norm[j];
             el = 0;
             ret = 0.0f;
         }
     }
+    cw = (cw & ~kElapsedMask) | ((uint32_t)el & kElapsedMask);
 
     if (valid) {
 #pragma unroll
-        for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = y1[j];
-        if (P.max_steps > 0 || (P.flags & RR_FLAG_EPISODE_STATS)) B.elapsed[i] = el;
-        if (P.flags & RR_FLAG_EPISODE_STATS) B.ep_ret[i] = ret;
-        io.reward[i] = r;
-        io.done[i] = (uint8_t)done;
-        if (io.truncated) io.truncated[i] = (uint8_t)trunc;
+        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
+        if (use_counter) bst_u(cw_r, cw, vo, 0);
+        if (P.flags & RR_FLAG_EPISODE_STATS) bst_f(ret_r, ret, vo, 0);
+        bst_f(make_rsrc(io.reward, plane), r, vo, 0);
+        bst_u8(make_rsrc(io.done, n), (uint8_t)done, i);
+        if (io.truncated) bst_u8(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
         if (io.terms) {
+            const rsrc_t tr = make_rsrc(io.terms, (uint64_t)(NT + 2) * plane);
 #pragma unroll
-            for (int j = 0; j < NT; ++j) io.terms[(int64_t)j * n + i] = t[j];
-            io.terms[(int64_t)NT * n + i] = bv ? 1.0f : 0.0f;           // info["bounds_violation"]
-            io.terms[(int64_t)(NT + 1) * n + i] = event ? 1.0f : 0.0f;  // solve_ivp status == 1
+            for (int j = 0; j < NT; ++j) bst_f(tr, t[j], vo, j * plane);
+            bst_f(tr, bv ? 1.0f : 0.0f, vo, NT * plane);           // info["bounds_violation"]
+            bst_f(tr, event ? 1.0f : 0.0f, vo, (NT + 1) * plane);  // solve_ivp status == 1
         }
     }
-    store_obs_tile<NS>(lds[wv], o, io.obs, wave_base, lane, n, io.obs_vec_ok);
+    const uint32_t nvalid = (n - wave_base) < (uint32_t)kWave ? (n - wave_base) : (uint32_t)kWave;
+    store_obs_tile<NS>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
+                       io.obs_vec_ok);
 }
 
 template <int MODEL>
@@ -579,15 +704,13 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
     const int64_t n = B.n;
     float s[NS], v0;
     if (mask == nullptr || mask[i]) {
-        uint4* rs = reinterpret_cast<uint4*>(B.rng) + i;
-        uint4 st = *rs;
-        Rng g{st.x, st.y, st.z, st.w};
+        const uint32_t ep = (B.counter[i] >> kEpisodeShift) + 1u;
+        Rng g = reset_rng(P.seed, P.id_off + i, ep, B.state[i], B.state[(int64_t)(NS - 1) * n + i]);
         sample_ic<MODEL>(P, g, s, v0);
-        *rs = make_uint4(g.s0, g.s1, g.s2, g.s3);
 #pragma unroll
         for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = s[j];
         B.v0[i] = v0;
-        B.elapsed[i] = 0;
+        B.counter[i] = ep << kEpisodeShift;
         B.ep_ret[i] = 0.0f;
     } else {
 #pragma unroll
@@ -611,17 +734,6 @@ __global__ __launch_bounds__(kBlock) void gather_done_kernel(const int32_t* idx,
     for (int j = 0; j < ns; ++j) g_obs[k * ns + j] = term_obs[i * ns + j];
     g_ret[k] = term_ret[i];
     g_len[k] = term_len[i];
-}
-
-__global__ __launch_bounds__(kBlock) void seed_kernel(uint32_t* rng, int64_t n, int64_t id_off, uint64_t seed)
-{
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    uint64_t x = seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(id_off + i + 1));
-    uint64_t a = splitmix64(x), b = splitmix64(x);
-    uint4 st = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-    if ((st.x | st.y | st.z | st.w) == 0u) st.x = 1u;
-    reinterpret_cast<uint4*>(rng)[i] = st;
 }
 
 // ---------------------------------------------------------------------------
@@ -701,17 +813,8 @@ KParams make_kparams(const rr_params& p)
     }
     k.omega_lt = ceil_f((double)p.omega_lim[0]);
     k.zero_h = floor_f(1e-3);
-    k.dm = (float)(-1.0 / (9.81 * kIsp));
-    k.jinv[0] = (float)(1.0 / kJ1);
-    k.jinv[1] = (float)(1.0 / kJ2);
-    k.jinv[2] = (float)(1.0 / kJ3);
-    k.jd[0] = (float)(kJ3 - kJ2);
-    k.jd[1] = (float)(kJ1 - kJ3);
-    k.jd[2] = (float)(kJ2 - kJ1);
-    k.rt15 = (float)(-kRT);
-    k.drag3 = (float)kDrag3;
-    k.lever_over_i3 = (float)(kLever3 / kI3);
-    k.zeta_hint = (float)(pi / 2);
+    k.seed = 42;
+    k.id_off = 0;
     return k;
 }
 
@@ -726,8 +829,7 @@ struct rr_env {
     uint64_t steps;
     float* state;
     float* v0;
-    int32_t* elapsed;
-    uint32_t* rng;
+    uint32_t* counter;
     float* ep_ret;
     uint64_t* done_bits;
     float* term_obs;
@@ -746,15 +848,13 @@ Bufs bufs_of(const rr_env* e)
     Bufs b;
     b.state = e->state;
     b.v0 = e->v0;
-    b.elapsed = e->elapsed;
-    b.rng = e->rng;
+    b.counter = e->counter;
     b.ep_ret = e->ep_ret;
     b.done_bits = e->done_bits;
     b.term_obs = e->term_obs;
     b.term_ret = e->term_ret;
     b.term_len = e->term_len;
     b.n = e->n;
-    b.id_off = e->id_off;
     return b;
 }
 
@@ -790,7 +890,11 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         return fail(RR_EINVAL, "rr_create: model must be 3 or 6");
     if (p->integrator != RR_INT_RK4 && p->integrator != RR_INT_EULER)
         return fail(RR_EINVAL, "rr_create: unknown integrator");
-    if (n <= 0 || n > (int64_t)INT32_MAX) return fail(RR_EINVAL, "rr_create: n must be in [1, 2^31)");
+    const int64_t ns_ = p->model == RR_MODEL_6DOF ? 14 : 7;
+    if (n <= 0 || n * ns_ * 4 > (int64_t)0xFFFFFFFF)
+        return fail(RR_EINVAL, "rr_create: n must be >= 1 and n*state_dim*4 must fit 32-bit buffer offsets");
+    if (p->max_episode_steps < 0 || p->max_episode_steps > (int32_t)kElapsedMask)
+        return fail(RR_EINVAL, "rr_create: max_episode_steps must be in [0, 65535]");
     if (!(p->dt > 0.0f)) return fail(RR_EINVAL, "rr_create: dt must be > 0");
     rr_env* e = new (std::nothrow) rr_env();
     if (!e) return fail(RR_ENOMEM, "rr_create: host allocation failed");
@@ -808,7 +912,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         size_t bytes;
     } allocs[] = {
         {(void**)&e->state, sizeof(float) * e->ns * n},   {(void**)&e->v0, sizeof(float) * n},
-        {(void**)&e->elapsed, sizeof(int32_t) * n},       {(void**)&e->rng, sizeof(uint32_t) * 4 * n},
+        {(void**)&e->counter, sizeof(uint32_t) * n},
         {(void**)&e->ep_ret, sizeof(float) * n},          {(void**)&e->done_bits, sizeof(uint64_t) * n_words(n)},
         {(void**)&e->term_obs, sizeof(float) * e->ns * n},
         {(void**)&e->term_ret, sizeof(float) * n},        {(void**)&e->term_len, sizeof(int32_t) * n},
@@ -827,6 +931,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
             return hip_fail(err, "rr_create: hipMemset");
         }
     }
+    e->kp.id_off = env_id_offset;
     int rc = rr_seed(e, 42, nullptr);
     if (rc == RR_OK) {
         hipError_t err = hipDeviceSynchronize();
@@ -844,7 +949,7 @@ int rr_destroy(rr_env* e)
 {
     if (!e) return RR_OK;
     DeviceGuard g(e->device);
-    void* ptrs[] = {e->state,    e->v0,       e->elapsed,  e->rng,   e->ep_ret, e->done_bits,
+    void* ptrs[] = {e->state,    e->v0,       e->counter,  e->ep_ret, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -858,11 +963,10 @@ int rr_action_dim(const rr_env* e) { return e ? e->na : -1; }
 
 int rr_seed(rr_env* e, uint64_t seed, void* stream)
 {
+    (void)stream;  // the reset stream is counter-based: the seed is a kernel argument
     if (!e) return fail(RR_EINVAL, "rr_seed: null handle");
-    hipLaunchKernelGGL(seed_kernel, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->rng, e->n,
-                       e->id_off, seed);
-    hipError_t err = hipGetLastError();
-    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_seed: launch");
+    e->kp.seed = seed;
+    return RR_OK;
 }
 
 int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
@@ -915,8 +1019,8 @@ int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32
     if (err == hipSuccess && v0)
         err = hipMemcpyAsync(e->v0, v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
     if (err == hipSuccess) {
-        if (elapsed) err = hipMemcpyAsync(e->elapsed, elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
-        else err = hipMemsetAsync(e->elapsed, 0, sizeof(int32_t) * e->n, s);
+        if (elapsed) err = hipMemcpyAsync(e->counter, elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+        else err = hipMemsetAsync(e->counter, 0, sizeof(int32_t) * e->n, s);
     }
     if (err == hipSuccess) err = hipMemsetAsync(e->ep_ret, 0, sizeof(float) * e->n, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_set_state");
@@ -931,7 +1035,7 @@ int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void*
         err = hipMemcpyAsync(state_soa, e->state, sizeof(float) * e->ns * e->n, hipMemcpyDeviceToDevice, s);
     if (err == hipSuccess && v0) err = hipMemcpyAsync(v0, e->v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
     if (err == hipSuccess && elapsed)
-        err = hipMemcpyAsync(elapsed, e->elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+        err = hipMemcpyAsync(elapsed, e->counter, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_get_state");
 }
 
@@ -940,7 +1044,7 @@ int rr_get_buffers(rr_env* e, rr_buffers* out)
     if (!e || !out) return fail(RR_EINVAL, "rr_get_buffers: null argument");
     out->state = e->state;
     out->v0 = e->v0;
-    out->elapsed = e->elapsed;
+    out->elapsed = (int32_t*)e->counter;
     out->ep_return = e->ep_ret;
     out->done_bits = e->done_bits;
     out->terminal_obs = e->term_obs;
