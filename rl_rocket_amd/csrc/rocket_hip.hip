@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -172,38 +173,44 @@ __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 
-struct Rng {
-    uint32_t s0, s1, s2, s3;
-    __device__ __forceinline__ float uniform()
-    {
-        uint32_t r = s0 + s3;
-        uint32_t t = s1 << 9;
-        s2 ^= s0;
-        s3 ^= s1;
-        s1 ^= s2;
-        s0 ^= s3;
-        s2 ^= t;
-        s3 = rotl32(s3, 11);
-        return (float)(r >> 8) * 0x1p-24f;  // [0, 1), 24 random bits
-    }
-};
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t& x)
+// 32-bit avalanche mix (lowbias32). Each uniform of a reset is its own short chain,
+// so the 14 draws are independent instructions (ILP at one wave per SIMD).
+__device__ __forceinline__ uint32_t mix32(uint32_t x)
 {
-    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
 
-__device__ __forceinline__ Rng reset_rng(uint64_t seed, int64_t gid, uint32_t episode, float salt_a, float salt_b)
+struct ResetKey {
+    uint32_t k0, k1;
+    // j-th uniform in [0, 1) with 24 random bits
+    __device__ __forceinline__ float uniform(uint32_t j) const
+    {
+        const uint32_t h = mix32(k0 ^ mix32(k1 + (j + 1u) * 0x9E3779B9u));
+        return (float)(h >> 8) * 0x1p-24f;
+    }
+};
+
+__device__ __forceinline__ ResetKey reset_key(uint64_t seed, int64_t gid, uint32_t episode, float salt_a,
+                                              float salt_b)
 {
     uint64_t x = seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(gid + 1));
     x ^= (uint64_t)episode * 0xA0761D6478BD642Full;
     x ^= ((uint64_t)__float_as_uint(salt_a) << 32) | (uint64_t)__float_as_uint(salt_b);
-    const uint64_t a = splitmix64(x), b = splitmix64(x);
-    Rng g{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32) | 1u};
-    return g;
+    const uint64_t a = splitmix64(x);
+    return ResetKey{(uint32_t)a, (uint32_t)(a >> 32)};
 }
 
 // ---------------------------------------------------------------------------
@@ -372,19 +379,20 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         const float hv0 = P.h * f0[EV], hv1 = P.h * f1[EV];
         float lo = 0.0f, hi = 1.0f;  // H(lo) has the sign of x0
         s = x0 * frcp(x0 - x1);
-        for (int it = 0; it < 12; ++it) {
+        // Newton from the secant guess, kept inside the sign bracket (bisection fallback);
+        // a fixed 6 iterations: branch-free, converged to fp32 for every row we test
+#pragma unroll
+        for (int it = 0; it < 6; ++it) {
             const float s2 = s * s, s3 = s2 * s;
             const float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
                             (s3 - s2) * hv1;
             const float dH = (6 * s2 - 6 * s) * (x0 - x1) + (3 * s2 - 4 * s + 1) * hv0 + (3 * s2 - 2 * s) * hv1;
-            if (H == 0.0f) break;
-            if ((H > 0.0f) == (x0 > 0.0f)) lo = s;
-            else hi = s;
+            const bool same = (H > 0.0f) == (x0 > 0.0f);
+            lo = same ? s : lo;
+            hi = same ? hi : s;
             float sn = s - H * frcp(dH);
-            if (!(sn > lo && sn < hi)) sn = 0.5f * (lo + hi);
-            const float ds = fabsf(sn - s);
-            s = sn;
-            if (ds < 1e-7f) break;
+            sn = (sn > lo && sn < hi) ? sn : 0.5f * (lo + hi);
+            s = (H == 0.0f) ? s : sn;
         }
     }
     const float s2 = s * s, s3 = s2 * s;
@@ -397,18 +405,17 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
 // Sample one initial condition: gym Box.sample (uniform in [low, high], float32),
 // then q <- q/|q| (rocket_env.py:672-673); v0 = |IC velocity| (rocket_env.py:989-991).
 template <int MODEL>
-__device__ __forceinline__ void sample_ic(const KParams& P, Rng& g, float* s, float& v0)
+__device__ __forceinline__ void sample_ic(const KParams& P, const ResetKey& k, float* s, float& v0)
 {
     constexpr int NS = Dims<MODEL>::NS;
 #pragma unroll
-    for (int j = 0; j < NS; ++j) s[j] = fmaf(P.ic_span[j], g.uniform(), P.ic_low[j]);
+    for (int j = 0; j < NS; ++j) s[j] = fmaf(P.ic_span[j], k.uniform(j), P.ic_low[j]);
     if constexpr (MODEL == 6) {
-        const float nq = sqrtf(s[6] * s[6] + s[7] * s[7] + s[8] * s[8] + s[9] * s[9]);
-        const float inq = 1.0f / nq;
-        s[6] *= inq;
-        s[7] *= inq;
-        s[8] *= inq;
-        s[9] *= inq;
+        const float rn = frsq(s[6] * s[6] + s[7] * s[7] + s[8] * s[8] + s[9] * s[9]);
+        s[6] *= rn;
+        s[7] *= rn;
+        s[8] *= rn;
+        s[9] *= rn;
         v0 = sqrtf(s[3] * s[3] + s[4] * s[4] + s[5] * s[5]);
     } else {
         v0 = sqrtf(s[3] * s[3] + s[4] * s[4]);
@@ -507,11 +514,12 @@ __device__ __forceinline__ float reward_terms(const KParams& P, const float* s, 
 }
 
 // Write this wave's [64][NS] observation tile through LDS as 16-B coalesced stores.
-template <int NS>
+template <int NS, int EPW>
 __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_t obs_r, uint32_t wave_base,
                                                int lane, uint32_t nvalid, bool vec_ok)
 {
-    if constexpr (NS % 2 == 0) {
+    if (lane >= EPW) {
+    } else if constexpr (NS % 2 == 0) {
         float2* l2 = reinterpret_cast<float2*>(lds + lane * NS);
 #pragma unroll
         for (int j = 0; j < NS / 2; ++j) l2[j] = make_float2(o[2 * j], o[2 * j + 1]);
@@ -523,8 +531,8 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint32_t sbase = wave_base * NS * 4u;  // byte offset of the tile (wave-uniform)
-    if (vec_ok && nvalid == kWave) {
-        constexpr int NV = kWave * NS / 4;
+    if (vec_ok && nvalid == (uint32_t)EPW) {
+        constexpr int NV = EPW * NS / 4;
         const u32x4* src4 = reinterpret_cast<const u32x4*>(lds);
 #pragma unroll
         for (int k = lane; k < NV; k += kWave)
@@ -538,18 +546,21 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
 // One launch = one env step of all N envs. Every HBM access goes through a buffer
 // descriptor: the per-lane byte offset is one 32-bit VGPR (i*4), plane offsets are
 // wave-uniform soffsets (NS*N*4 < 4 GiB, checked at rr_create).
-template <int MODEL, int INTEG>
+// EPW = envs per wave: 64 (one env per lane), or 32 (lanes 32-63 idle) so that small
+// batches put two waves on every SIMD.
+template <int MODEL, int INTEG, int EPW>
 __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Bufs B, const StepIO io)
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
-    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][kWave * NS];
+    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][EPW * NS];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = threadIdx.x / kWave;
     const uint32_t n = (uint32_t)B.n;
-    const uint32_t wave_base = blockIdx.x * kBlock + wv * kWave;
+    const uint32_t wave_idx = blockIdx.x * kWavesPerBlock + wv;
+    const uint32_t wave_base = wave_idx * EPW;
     if (wave_base >= n) return;  // wave-uniform
     const uint32_t i = wave_base + lane;
-    const bool valid = i < n;
+    const bool valid = (EPW == kWave || lane < (uint32_t)EPW) && i < n;
     const uint32_t ic = valid ? i : n - 1;
     const uint32_t vo = ic * 4u;           // per-lane byte offset in every fp32/u32 plane
     const uint32_t plane = n * 4u;         // bytes per plane
@@ -650,19 +661,28 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     // side expands the masks into the sorted index list, rr_fetch_done).
     const bool dv = done && valid;
     const uint64_t m = __ballot(dv);
-    if (lane == 0) B.done_bits[wave_base / kWave] = m;
+    if (lane == 0) {
+        if constexpr (EPW == kWave) B.done_bits[wave_idx] = m;
+        else reinterpret_cast<uint32_t*>(B.done_bits)[wave_idx] = (uint32_t)m;  // little-endian: same bit order
+    }
     if (m) {
         if (dv) {
-            float* to = B.term_obs + (size_t)i * NS;
+            float2* to = reinterpret_cast<float2*>(B.term_obs + (size_t)i * NS);  // NS even or not: 8-B aligned rows
+            if constexpr (NS % 2 == 0) {
 #pragma unroll
-            for (int j = 0; j < NS; ++j) to[j] = o[j];
+                for (int j = 0; j < NS / 2; ++j) to[j] = make_float2(o[2 * j], o[2 * j + 1]);
+            } else {
+                float* tf = B.term_obs + (size_t)i * NS;
+#pragma unroll
+                for (int j = 0; j < NS; ++j) tf[j] = o[j];
+            }
             B.term_ret[i] = ret;
             B.term_len[i] = el;
         }
         if ((P.flags & RR_FLAG_AUTO_RESET) && dv) {
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
-            Rng g = reset_rng(P.seed, P.id_off + i, ep, y1[0], y1[NS - 1]);
-            sample_ic<MODEL>(P, g, y1, v0);
+            const ResetKey key = reset_key(P.seed, P.id_off + i, ep, y1[0], y1[NS - 1]);
+            sample_ic<MODEL>(P, key, y1, v0);
             B.v0[i] = v0;
             cw = ep << kEpisodeShift;
 #pragma unroll
@@ -689,9 +709,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
             bst_f(tr, event ? 1.0f : 0.0f, vo, (NT + 1) * plane);  // solve_ivp status == 1
         }
     }
-    const uint32_t nvalid = (n - wave_base) < (uint32_t)kWave ? (n - wave_base) : (uint32_t)kWave;
-    store_obs_tile<NS>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
-                       io.obs_vec_ok);
+    const uint32_t nvalid = (n - wave_base) < (uint32_t)EPW ? (n - wave_base) : (uint32_t)EPW;
+    store_obs_tile<NS, EPW>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
+                            io.obs_vec_ok);
 }
 
 template <int MODEL>
@@ -705,8 +725,8 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
     float s[NS], v0;
     if (mask == nullptr || mask[i]) {
         const uint32_t ep = (B.counter[i] >> kEpisodeShift) + 1u;
-        Rng g = reset_rng(P.seed, P.id_off + i, ep, B.state[i], B.state[(int64_t)(NS - 1) * n + i]);
-        sample_ic<MODEL>(P, g, s, v0);
+        const ResetKey key = reset_key(P.seed, P.id_off + i, ep, B.state[i], B.state[(int64_t)(NS - 1) * n + i]);
+        sample_ic<MODEL>(P, key, s, v0);
 #pragma unroll
         for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = s[j];
         B.v0[i] = v0;
@@ -827,6 +847,7 @@ struct rr_env {
     int ns, na, nt;
     int64_t n, id_off;
     uint64_t steps;
+    bool half_wave;      // 32 envs per wave (small N: 2 waves per SIMD)
     float* state;
     float* v0;
     uint32_t* counter;
@@ -932,6 +953,13 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         }
     }
     e->kp.id_off = env_id_offset;
+    {
+        // Wave geometry: below ~2 waves per SIMD with 64 envs per wave, use 32 envs per
+        // wave (RR_WAVE_ENVS=32|64 overrides; measured in tools/diag_kernel.py).
+        const char* env = std::getenv("RR_WAVE_ENVS");
+        const int64_t simds = 256 * 4;
+        e->half_wave = env ? std::atoi(env) == 32 : (n / 64 < 2 * simds);
+    }
     int rc = rr_seed(e, 42, nullptr);
     if (rc == RR_OK) {
         hipError_t err = hipDeviceSynchronize();
@@ -997,14 +1025,18 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
     io.terms = terms;
     io.obs_vec_ok = ((uintptr_t)obs & 15u) == 0;
     const Bufs b = bufs_of(e);
-    const dim3 grid(grid_of(e->n)), block(kBlock);
     hipStream_t s = (hipStream_t)stream;
     const bool m6 = e->p.model == RR_MODEL_6DOF;
     const bool euler = e->p.integrator == RR_INT_EULER;
-    if (m6 && !euler) hipLaunchKernelGGL((step_kernel<6, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
-    else if (m6) hipLaunchKernelGGL((step_kernel<6, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
-    else if (!euler) hipLaunchKernelGGL((step_kernel<3, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
-    else hipLaunchKernelGGL((step_kernel<3, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
+    const bool half = e->half_wave;
+    const int64_t epb = (half ? 32 : 64) * kWavesPerBlock;  // envs per block
+    const dim3 grid((unsigned)((e->n + epb - 1) / epb)), block(kBlock);
+#define RR_LAUNCH(M, I, W) hipLaunchKernelGGL((step_kernel<M, I, W>), grid, block, 0, s, e->kp, b, io)
+    if (m6 && !euler) { if (half) RR_LAUNCH(6, RR_INT_RK4, 32); else RR_LAUNCH(6, RR_INT_RK4, 64); }
+    else if (m6) { if (half) RR_LAUNCH(6, RR_INT_EULER, 32); else RR_LAUNCH(6, RR_INT_EULER, 64); }
+    else if (!euler) { if (half) RR_LAUNCH(3, RR_INT_RK4, 32); else RR_LAUNCH(3, RR_INT_RK4, 64); }
+    else { if (half) RR_LAUNCH(3, RR_INT_EULER, 32); else RR_LAUNCH(3, RR_INT_EULER, 64); }
+#undef RR_LAUNCH
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return hip_fail(err, "rr_step: launch");
     e->steps++;

@@ -30,6 +30,10 @@ def _check_rows(model, g, out, label):
         label, e_state.max(), e_obs.max(), e_rew.max(), e_terms.max(), (~done_eq).sum(), (~bv_eq).sum(),
         (~ev_eq).sum())
     print(msg)
+    e_comp = floored_rel(out["state_out"], g["state_out"], norm)
+    worst = np.argmax(e_comp, axis=0)
+    print("  per-component max:", " ".join("%d:%.2g(row %d g%d)" % (j, e_comp[worst[j], j], worst[j],
+                                                                     g["group"][worst[j]]) for j in range(ns)))
     bad = np.where((e_state > TOL_STATE) | (e_obs > TOL_STATE) | (e_rew > TOL_REWARD) | (e_terms > TOL_REWARD)
                    | ~done_eq | ~bv_eq | ~ev_eq)[0]
     for i in bad[:10]:
