@@ -21,7 +21,6 @@
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
-#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -379,10 +378,11 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         const float hv0 = P.h * f0[EV], hv1 = P.h * f1[EV];
         float lo = 0.0f, hi = 1.0f;  // H(lo) has the sign of x0
         s = x0 * frcp(x0 - x1);
-        // Newton from the secant guess, kept inside the sign bracket (bisection fallback);
-        // a fixed 6 iterations: branch-free, converged to fp32 for every row we test
+        // Newton from the secant guess, kept inside the closed sign bracket [lo, hi]
+        // (bisection fallback). A converged iterate sits on a bracket end, so the test is
+        // inclusive. Fixed 8 iterations, branch-free.
 #pragma unroll
-        for (int it = 0; it < 6; ++it) {
+        for (int it = 0; it < 8; ++it) {
             const float s2 = s * s, s3 = s2 * s;
             const float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
                             (s3 - s2) * hv1;
@@ -391,7 +391,7 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
             lo = same ? s : lo;
             hi = same ? hi : s;
             float sn = s - H * frcp(dH);
-            sn = (sn > lo && sn < hi) ? sn : 0.5f * (lo + hi);
+            sn = (sn >= lo && sn <= hi) ? sn : 0.5f * (lo + hi);
             s = (H == 0.0f) ? s : sn;
         }
     }
@@ -546,9 +546,9 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
 // One launch = one env step of all N envs. Every HBM access goes through a buffer
 // descriptor: the per-lane byte offset is one 32-bit VGPR (i*4), plane offsets are
 // wave-uniform soffsets (NS*N*4 < 4 GiB, checked at rr_create).
-// EPW = envs per wave: 64 (one env per lane), or 32 (lanes 32-63 idle) so that small
-// batches put two waves on every SIMD.
-template <int MODEL, int INTEG, int EPW>
+// EPW = envs per wave (one env per lane). 32 envs per wave (half-empty waves, two per
+// SIMD at N = 65536) was measured slower at every N (tools/diag_kernel.py).
+template <int MODEL, int INTEG, int EPW = kWave>
 __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Bufs B, const StepIO io)
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
@@ -847,7 +847,6 @@ struct rr_env {
     int ns, na, nt;
     int64_t n, id_off;
     uint64_t steps;
-    bool half_wave;      // 32 envs per wave (small N: 2 waves per SIMD)
     float* state;
     float* v0;
     uint32_t* counter;
@@ -953,13 +952,6 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         }
     }
     e->kp.id_off = env_id_offset;
-    {
-        // Wave geometry: below ~2 waves per SIMD with 64 envs per wave, use 32 envs per
-        // wave (RR_WAVE_ENVS=32|64 overrides; measured in tools/diag_kernel.py).
-        const char* env = std::getenv("RR_WAVE_ENVS");
-        const int64_t simds = 256 * 4;
-        e->half_wave = env ? std::atoi(env) == 32 : (n / 64 < 2 * simds);
-    }
     int rc = rr_seed(e, 42, nullptr);
     if (rc == RR_OK) {
         hipError_t err = hipDeviceSynchronize();
@@ -1028,15 +1020,11 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
     hipStream_t s = (hipStream_t)stream;
     const bool m6 = e->p.model == RR_MODEL_6DOF;
     const bool euler = e->p.integrator == RR_INT_EULER;
-    const bool half = e->half_wave;
-    const int64_t epb = (half ? 32 : 64) * kWavesPerBlock;  // envs per block
-    const dim3 grid((unsigned)((e->n + epb - 1) / epb)), block(kBlock);
-#define RR_LAUNCH(M, I, W) hipLaunchKernelGGL((step_kernel<M, I, W>), grid, block, 0, s, e->kp, b, io)
-    if (m6 && !euler) { if (half) RR_LAUNCH(6, RR_INT_RK4, 32); else RR_LAUNCH(6, RR_INT_RK4, 64); }
-    else if (m6) { if (half) RR_LAUNCH(6, RR_INT_EULER, 32); else RR_LAUNCH(6, RR_INT_EULER, 64); }
-    else if (!euler) { if (half) RR_LAUNCH(3, RR_INT_RK4, 32); else RR_LAUNCH(3, RR_INT_RK4, 64); }
-    else { if (half) RR_LAUNCH(3, RR_INT_EULER, 32); else RR_LAUNCH(3, RR_INT_EULER, 64); }
-#undef RR_LAUNCH
+    const dim3 grid(grid_of(e->n)), block(kBlock);
+    if (m6 && !euler) hipLaunchKernelGGL((step_kernel<6, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
+    else if (m6) hipLaunchKernelGGL((step_kernel<6, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
+    else if (!euler) hipLaunchKernelGGL((step_kernel<3, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
+    else hipLaunchKernelGGL((step_kernel<3, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return hip_fail(err, "rr_step: launch");
     e->steps++;

@@ -87,9 +87,6 @@ def main():
         subprocess.check_call(cmd)
         for n in [int(x) for x in args.ns.split(",")]:
             env = dict(os.environ, RR_LIB_PATH=lib)
-            for w in ("w32", "w64"):
-                if w in v:
-                    env["RR_WAVE_ENVS"] = w[1:]
             cmd = [sys.executable, __file__, "--child", "--tag", "diag%s" % v, "--n", str(n), "--model",
                    str(args.model), "--integrator", args.integrator, "--steps", str(args.steps)]
             r = subprocess.run(cmd, env=env, timeout=300)
