@@ -125,17 +125,15 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
     pool = torch.rand((POOL, n, env.action_dim), device=dev, generator=gen) * 2 - 1
-    if args.allgather:
-        g_obs = torch.empty((world * n, env.state_dim), device=dev)
-        g_rew = torch.empty((world * n,), device=dev)
-        g_done = torch.empty((world * n,), device=dev, dtype=torch.uint8)
+    gather = None
+    if args.allgather and dist is not None:
+        from rl_rocket_amd.dist import ShardGather
+        gather = ShardGather(n, env.state_dim, dev)
 
     def one(k):
         obs, rew, done, _ = env.step(pool[k % POOL])
-        if args.allgather and dist is not None:
-            dist.all_gather_into_tensor(g_obs, obs)
-            dist.all_gather_into_tensor(g_rew, rew)
-            dist.all_gather_into_tensor(g_done, done)
+        if gather is not None:
+            gather(obs, rew, done)  # RCCL all_gather over xGMI: global batch on every rank
 
     stream = torch.cuda.current_stream(dev)
     for k in range(args.warmup):
