@@ -98,6 +98,19 @@ def cpu_baseline(model, seconds, seed=0):
                       "container (BASELINE.md)" % (steps, "6DOF" if model == 6 else "3DOF", n, steps // n)}
 
 
+def stored_traffic(model, n):
+    """Per-launch HBM bytes of the same kernel/config from the latest committed rocprofv3 PMC
+    passes (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or (None, None)."""
+    import glob
+
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_n%d.json" % n)))
+    for path in reversed(hits):
+        d = json.load(open(path))
+        if d.get("kernel", "").startswith("step_kernel<%d," % model):
+            return d["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -186,6 +199,7 @@ def main():
     value = n * world * K / dt
     bytes_launch = BYTES_PER_STEP[model] * n
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = stored_traffic(model, n)
     result = {
         "metric": "env-steps/sec (%s, N=%d per GPU)" % ("6DOF" if model == 6 else "3DOF", n),
         "value": value,
@@ -208,7 +222,8 @@ def main():
                    "graph_steps": gs if use_graph else 0,
                    "parallelism": "env-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "B/launch",
+                     "traffic_source": traffic_src,
                      "kernel": "step_kernel<%d,%s>" % (model, args.integrator.upper()),
                      "kernel_us": kern_ms * 1e3, "bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": BYTES_PER_STEP[model]},
