@@ -164,6 +164,16 @@ __device__ __forceinline__ const T& at(const T* base, uint32_t idx)
     return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (uint32_t)(idx * (uint32_t)sizeof(T)));
 }
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }  // v_sqrt_f32, no IEEE fixup
+
+// 1 - exp(-x) for x >= 0 without cancellation: Taylor series below 1/8 (truncation
+// < 2e-9 relative), v_exp_f32 above (result >= 0.117, so its ulp error stays relative).
+__device__ __forceinline__ float one_minus_exp_neg(float x)
+{
+    const float p = x * (1.0f - x * (0.5f - x * (1.0f / 6.0f - x * (1.0f / 24.0f - x * (1.0f / 120.0f)))));
+    const float e = 1.0f - __builtin_amdgcn_exp2f(-x * 1.44269504088896341f);
+    return x < 0.125f ? p : e;
+}
 
 // ---------------------------------------------------------------------------
 // Reset stream: counter-based. A reset of env `gid` in its episode `ep` seeds a
@@ -197,7 +207,7 @@ struct ResetKey {
     // j-th uniform in [0, 1) with 24 random bits
     __device__ __forceinline__ float uniform(uint32_t j) const
     {
-        const uint32_t h = mix32(k0 ^ mix32(k1 + (j + 1u) * 0x9E3779B9u));
+        const uint32_t h = mix32(k0 + (j + 1u) * 0x9E3779B9u) ^ k1;
         return (float)(h >> 8) * 0x1p-24f;
     }
 };
@@ -380,9 +390,10 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         s = x0 * frcp(x0 - x1);
         // Newton from the secant guess, kept inside the closed sign bracket [lo, hi]
         // (bisection fallback). A converged iterate sits on a bracket end, so the test is
-        // inclusive. Fixed 8 iterations, branch-free.
+        // inclusive. Fixed 5 iterations, branch-free (quadratic convergence from the secant
+        // guess; the parity tests cover touchdowns down to |v| ~ 1 m/s).
 #pragma unroll
-        for (int it = 0; it < 8; ++it) {
+        for (int it = 0; it < 5; ++it) {
             const float s2 = s * s, s3 = s2 * s;
             const float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
                             (s3 - s2) * hv1;
@@ -416,9 +427,9 @@ __device__ __forceinline__ void sample_ic(const KParams& P, const ResetKey& k, f
         s[7] *= rn;
         s[8] *= rn;
         s[9] *= rn;
-        v0 = sqrtf(s[3] * s[3] + s[4] * s[4] + s[5] * s[5]);
+        v0 = fsqrt(s[3] * s[3] + s[4] * s[4] + s[5] * s[5]);
     } else {
-        v0 = sqrtf(s[3] * s[3] + s[4] * s[4]);
+        v0 = fsqrt(s[3] * s[3] + s[4] * s[4]);
     }
 }
 
@@ -443,12 +454,12 @@ __device__ __forceinline__ float reward_terms(const KParams& P, const float* s, 
             vh0 = s[3] + 1.0f;
             tau_inv = 1.0f / 100.0f;
         }
-        float nrh = sqrtf(rh0 * rh0 + rh1 * rh1 + rh2 * rh2);
-        float nvh = sqrtf(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
+        float nrh = fsqrt(rh0 * rh0 + rh1 * rh1 + rh2 * rh2);
+        float nvh = fsqrt(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
         float t_go = nrh * frcp(nvh);
-        float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * (-expm1f(-t_go * tau_inv));
+        float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * one_minus_exp_neg(t_go * tau_inv);
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
-        t[0] = P.alfa * sqrtf(e0 * e0 + e1 * e1 + e2 * e2);
+        t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1 + e2 * e2);
         // thrust_penalty = beta * T (denormalised, float32)
         t[1] = P.beta * ((a[2] + 1.0f) * P.half_thrust);
         t[2] = P.eta;
@@ -461,8 +472,8 @@ __device__ __forceinline__ float reward_terms(const KParams& P, const float* s, 
         float R02 = 2.0f * (x * z + y * w);
         float mR12 = 2.0f * (x * w - y * z);
         float R22 = w * w - x * x - y * y + z * z;
-        float ra = sqrtf(R00 * R00 + mR01 * mR01);
-        float rc = sqrtf(R22 * R22 + mR12 * mR12);
+        float ra = fsqrt(R00 * R00 + mR01 * mR01);
+        float rc = fsqrt(R22 * R22 + mR12 * mR12);
         float sb = fabsf(R02) / qq;
         bool att = (!(P.att_never & 1u) && R00 < ra * P.att_c[0]) || (!(P.att_never & 2u) && sb > P.att_c[1]) ||
                    (!(P.att_never & 4u) && R22 < rc * P.att_c[2]);
@@ -491,12 +502,12 @@ __device__ __forceinline__ float reward_terms(const KParams& P, const float* s, 
             vh1 = s[4] + 1.0f;
             tau_inv = 1.0f / 100.0f;
         }
-        float nrh = sqrtf(rh0 * rh0 + rh1 * rh1);
-        float nvh = sqrtf(s[3] * s[3] + vh1 * vh1);
+        float nrh = fsqrt(rh0 * rh0 + rh1 * rh1);
+        float nvh = fsqrt(s[3] * s[3] + vh1 * vh1);
         float t_go = nrh * frcp(nvh);
-        float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * (-expm1f(-t_go * tau_inv));
+        float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * one_minus_exp_neg(t_go * tau_inv);
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1;
-        t[0] = P.alfa * sqrtf(e0 * e0 + e1 * e1);
+        t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1);
         t[1] = P.beta * ((a[1] + 1.0f) * P.half_thrust);
         t[2] = P.eta;
         float zeta = fabsf(s[2] - kHalfPi);

@@ -31,4 +31,10 @@ if [ -n "$PMC" ]; then
     ok_or_testfail $? pmc_$C
   done
 fi
+if [ -n "$SQ" ]; then
+  timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmc_SQ" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $PMC_ARGS > "$OUT/pmc_SQ.log" 2>&1
+  ok_or_testfail $? pmc_SQ
+  timeout -k 10 600 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmc_GRBM" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $PMC_ARGS > "$OUT/pmc_GRBM.log" 2>&1
+  ok_or_testfail $? pmc_GRBM
+fi
 echo done
