@@ -30,7 +30,8 @@
 
 // Diagnostic ablations (tools/diag_kernel.py only; the product build has RR_DIAG 0):
 //   1 = memory only (no integration / reward arithmetic), 2 = no event / reset branches,
-//   3 = compute only (state synthesised in registers instead of loaded).
+//   3 = compute only (state synthesised in registers instead of loaded),
+//   4 = product kernel + s_memtime phase stamps per wave (rr_debug_stamps).
 #ifndef RR_DIAG
 #define RR_DIAG 0
 #endif
@@ -96,6 +97,9 @@ struct KParams {
 };
 
 struct Bufs {
+#if RR_DIAG == 4
+    uint64_t* stamps;         // [waves][8]
+#endif
     float* state;
     float* v0;
     uint32_t* counter;        // [N] elapsed | episode << 16
@@ -118,6 +122,21 @@ struct StepIO {
 };
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+#if RR_DIAG == 4
+#define RR_STAMP(k)                                                                     \
+    do {                                                                                \
+        uint64_t t_;                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");    \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        stamp_[k] = t_;                                                                 \
+    } while (0)
+#else
+#define RR_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
 
 // Raw buffer access (SRSRC descriptor built from wave-uniform values): 32-bit per-lane
 // voffset, per-plane offsets in soffset (SGPR) — no per-lane 64-bit address arithmetic.
@@ -581,6 +600,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     const rsrc_t v0_r = make_rsrc(B.v0, plane);
     const rsrc_t cw_r = make_rsrc(B.counter, plane);
     const rsrc_t ret_r = make_rsrc(B.ep_ret, plane);
+#if RR_DIAG == 4
+    uint64_t stamp_[8];
+#endif
+    RR_STAMP(0);
 
     // ---- all loads first (one memory round trip per wave) ----
     float y0[NS], y1[NS], f0[NS], a[NA];
@@ -607,6 +630,17 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     float v0 = bld_f(v0_r, vo, 0);
     uint32_t cw = use_counter ? bld_u(cw_r, vo, 0) : 0u;
     float ret = (P.flags & RR_FLAG_EPISODE_STATS) ? bld_f(ret_r, vo, 0) : 0.0f;
+#if RR_DIAG == 4
+    {  // force every load to land, then stamp
+        float sum_ = v0 + (float)cw + ret;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) sum_ += y0[j];
+#pragma unroll
+        for (int j = 0; j < NA; ++j) sum_ += a[j];
+        asm volatile("" ::"v"(sum_));
+    }
+#endif
+    RR_STAMP(1);
 
 #if RR_DIAG == 1
 #pragma unroll
@@ -621,8 +655,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
 #else
     const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
 #endif
+    RR_STAMP(2);
     if (event) event_step<MODEL>(P, c, y0, f0, y1);
 #endif
+    RR_STAMP(3);
 
     if constexpr (MODEL == 6) {
         // _normalize_quaternion (simulator.py:250)
@@ -662,6 +698,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
         done = true;
     }
     ret += r;
+    RR_STAMP(4);
 
     float o[NS];
 #pragma unroll
@@ -703,6 +740,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
         }
     }
     cw = (cw & ~kElapsedMask) | ((uint32_t)el & kElapsedMask);
+    RR_STAMP(5);
 
     if (valid) {
 #pragma unroll
@@ -723,6 +761,15 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     const uint32_t nvalid = (n - wave_base) < (uint32_t)EPW ? (n - wave_base) : (uint32_t)EPW;
     store_obs_tile<NS, EPW>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
                             io.obs_vec_ok);
+    RR_STAMP(6);
+#if RR_DIAG == 4
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RR_STAMP(7);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 8 + k] = stamp_[k];
+    }
+#endif
 }
 
 template <int MODEL>
@@ -866,6 +913,9 @@ struct rr_env {
     float* term_obs;
     float* term_ret;
     int32_t* term_len;
+#if RR_DIAG == 4
+    uint64_t* stamps;
+#endif
     int32_t* g_idx;     // rr_fetch_done scratch
     float* g_obs;
     float* g_ret;
@@ -882,6 +932,9 @@ Bufs bufs_of(const rr_env* e)
     b.counter = e->counter;
     b.ep_ret = e->ep_ret;
     b.done_bits = e->done_bits;
+#if RR_DIAG == 4
+    b.stamps = e->stamps;
+#endif
     b.term_obs = e->term_obs;
     b.term_ret = e->term_ret;
     b.term_len = e->term_len;
@@ -949,6 +1002,9 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->term_ret, sizeof(float) * n},        {(void**)&e->term_len, sizeof(int32_t) * n},
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
+#if RR_DIAG == 4
+        {(void**)&e->stamps, sizeof(uint64_t) * 8 * n_words(n)},
+#endif
     };
     for (auto& a : allocs) {
         hipError_t err = hipMalloc(a.ptr, a.bytes);
@@ -1140,5 +1196,16 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
         err = hipMemcpyAsync(term_len, e->term_len, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_copy_terminal");
 }
+
+#if RR_DIAG == 4
+// diagnostic build only: copy the per-wave phase stamps of the last step to the host
+int64_t rr_debug_stamps(rr_env* e, uint64_t* host, int64_t cap)
+{
+    const int64_t nw = std::min<int64_t>(cap / 8, n_words(e->n));
+    hipError_t err = hipDeviceSynchronize();
+    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 8 * nw, hipMemcpyDeviceToHost);
+    return err == hipSuccess ? nw : hip_fail(err, "rr_debug_stamps");
+}
+#endif
 
 }  // extern "C"

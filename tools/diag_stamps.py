@@ -1,0 +1,74 @@
+"""Per-wave phase timeline of the step kernel (RR_DIAG=4 build, s_memtime stamps).
+
+    python tools/diag_stamps.py [--n 65536] [--steps 40]
+
+Phases (cycles, shader clock): 0->1 load burst landed, 1->2 RK4, 2->3 event path,
+3->4 reward/done, 4->5 done mask + reset, 5->6 stores issued, 6->7 stores drained.
+Diagnostic only: the stamps' waits serialise the wave, so read shares, not totals.
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "diag"))
+    a = ap.parse_args()
+    from rl_rocket_amd import build as b
+
+    os.makedirs(a.out, exist_ok=True)
+    lib_path = os.path.join(a.out, "librocket_hip_diag4.so")
+    subprocess.check_call(b.command(out=lib_path, defines=("RR_DIAG=4",)))
+    os.environ["RR_LIB_PATH"] = lib_path
+    import torch
+
+    from rl_rocket_amd import _lib
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+
+    lib = _lib.load()
+    lib.rr_debug_stamps.restype = ctypes.c_int64
+    lib.rr_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    env = RocketBatch(a.n, model=6, device="cuda:0", max_episode_steps=800, episode_stats=False, **ENV_CONFIG_6DOF)
+    env.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(3)
+    nw = (a.n + 63) // 64
+    buf = np.zeros(nw * 8, np.uint64)
+    rows = []
+    for k in range(a.steps):
+        env.step(torch.rand((a.n, 3), device="cuda:0", generator=g) * 2 - 1)
+        if k >= a.steps - 10:
+            lib.rr_debug_stamps(env._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+            rows.append(buf.reshape(nw, 8).astype(np.int64).copy())
+    st = np.concatenate(rows)
+    names = ["load", "rk4", "event", "reward", "done+reset", "store_issue", "store_drain"]
+    d = np.diff(st, axis=1)
+    out = {"n": a.n, "waves": int(nw), "samples": int(st.shape[0])}
+    for j, nm in enumerate(names):
+        out[nm] = {"median": float(np.median(d[:, j])), "p90": float(np.percentile(d[:, j], 90)),
+                   "max": float(d[:, j].max())}
+    per = st.reshape(len(rows), nw, 8)
+    start_skew = [float(np.percentile(p[:, 0] - p[:, 0].min(), 90)) for p in per]
+    total = [float(p[:, 7].max() - p[:, 0].min()) for p in per]
+    life = [float(np.median(p[:, 7] - p[:, 0])) for p in per]
+    out["start_skew_p90"] = float(np.median(start_skew))
+    out["kernel_span_cycles"] = float(np.median(total))
+    out["wave_life_median"] = float(np.median(life))
+    print(json.dumps(out, indent=1))
+    env.close()
+
+
+if __name__ == "__main__":
+    main()
