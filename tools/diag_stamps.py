@@ -37,6 +37,7 @@ def main():
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
 
+    _lib.LIB_PATH = lib_path
     lib = _lib.load()
     lib.rr_debug_stamps.restype = ctypes.c_int64
     lib.rr_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
