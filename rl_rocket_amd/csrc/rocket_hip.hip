@@ -666,6 +666,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     const rsrc_t ret_r = make_rsrc(B.ep_ret, plane);
 #if RR_DIAG == 4
     uint64_t stamp_[8];
+    const uint64_t rt0_ = __builtin_amdgcn_s_memrealtime();
 #endif
     RR_STAMP(0);
 
@@ -830,9 +831,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
 #if RR_DIAG == 4
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     RR_STAMP(7);
+    const uint64_t rt1_ = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 8 + k] = stamp_[k];
+        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 10 + k] = stamp_[k];
+        B.stamps[(size_t)wave_idx * 10 + 8] = rt0_;
+        B.stamps[(size_t)wave_idx * 10 + 9] = rt1_;
     }
 #endif
 }
@@ -1068,7 +1072,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
 #if RR_DIAG == 4
-        {(void**)&e->stamps, sizeof(uint64_t) * 8 * n_words(n)},
+        {(void**)&e->stamps, sizeof(uint64_t) * 10 * n_words(n)},
 #endif
     };
     for (auto& a : allocs) {
@@ -1266,9 +1270,9 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
 // diagnostic build only: copy the per-wave phase stamps of the last step to the host
 int64_t rr_debug_stamps(rr_env* e, uint64_t* host, int64_t cap)
 {
-    const int64_t nw = std::min<int64_t>(cap / 8, n_words(e->n));
+    const int64_t nw = std::min<int64_t>(cap / 10, n_words(e->n));
     hipError_t err = hipDeviceSynchronize();
-    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 8 * nw, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 10 * nw, hipMemcpyDeviceToHost);
     return err == hipSuccess ? nw : hip_fail(err, "rr_debug_stamps");
 }
 #endif

@@ -46,27 +46,30 @@ def main():
     g = torch.Generator(device="cuda:0")
     g.manual_seed(3)
     nw = (a.n + 63) // 64
-    buf = np.zeros(nw * 8, np.uint64)
+    buf = np.zeros(nw * 10, np.uint64)
     rows = []
     for k in range(a.steps):
         env.step(torch.rand((a.n, 3), device="cuda:0", generator=g) * 2 - 1)
         if k >= a.steps - 10:
             lib.rr_debug_stamps(env._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
-            rows.append(buf.reshape(nw, 8).astype(np.int64).copy())
-    st = np.concatenate(rows)
+            rows.append(buf.reshape(nw, 10).astype(np.int64).copy())
+    allst = np.concatenate(rows)
+    st = allst[:, :8]
     names = ["load", "rk4", "event", "reward", "done+reset", "store_issue", "store_drain"]
     d = np.diff(st, axis=1)
     out = {"n": a.n, "waves": int(nw), "samples": int(st.shape[0])}
     for j, nm in enumerate(names):
         out[nm] = {"median": float(np.median(d[:, j])), "p90": float(np.percentile(d[:, j], 90)),
                    "max": float(d[:, j].max())}
-    per = st.reshape(len(rows), nw, 8)
-    start_skew = [float(np.percentile(p[:, 0] - p[:, 0].min(), 90)) for p in per]
-    total = [float(p[:, 7].max() - p[:, 0].min()) for p in per]
-    life = [float(np.median(p[:, 7] - p[:, 0])) for p in per]
-    out["start_skew_p90"] = float(np.median(start_skew))
-    out["kernel_span_cycles"] = float(np.median(total))
-    out["wave_life_median"] = float(np.median(life))
+    per = allst.reshape(len(rows), nw, 10)
+    # realtime stamps: 100 MHz, one clock for every XCD -> dispatch skew and tail in us
+    rt = [(p[:, 8] - p[:, 8].min()) / 100.0 for p in per]
+    rte = [(p[:, 9] - p[:, 8].min()) / 100.0 for p in per]
+    out["start_us_p50_p90_max"] = [float(np.median([np.percentile(r, q) for r in rt])) for q in (50, 90, 100)]
+    out["end_us_p50_p90_max"] = [float(np.median([np.percentile(r, q) for r in rte])) for q in (50, 90, 100)]
+    out["wave_life_us_median"] = float(np.median([np.median(e - s) for s, e in zip(rt, rte)]))
+    out["wave_life_cycles_median"] = float(np.median(per[:, :, 7] - per[:, :, 0]))
+    out["clock_ghz"] = out["wave_life_cycles_median"] / out["wave_life_us_median"] / 1e3
     print(json.dumps(out, indent=1))
     env.close()
 
