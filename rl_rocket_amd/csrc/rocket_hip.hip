@@ -739,6 +739,20 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
         y1[2] = fmodf(th, kTwoPi);
     }
 
+    // ---- early stores: the post-step state and obs leave now, so their store burst
+    // drains under the reward / done / reset arithmetic below (envs that end this step
+    // are rewritten after their reset, a rare scattered write) ----
+    const uint32_t nvalid = (n - wave_base) < (uint32_t)EPW ? (n - wave_base) : (uint32_t)EPW;
+    const rsrc_t obs_r = make_rsrc(io.obs, (uint64_t)NS * plane);
+    float o[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) o[j] = y1[j] * H.inv_norm[j];
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
+    }
+    store_obs_tile<NS, EPW>(lds[wv], o, obs_r, wave_base, lane, nvalid, io.obs_vec_ok);
+
     bool bv;
     float t[NT];
 #if RR_DIAG == 1
@@ -765,10 +779,6 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     }
     ret += r;
     RR_STAMP(4);
-
-    float o[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) o[j] = y1[j] * H.inv_norm[j];
 
     // Done compaction: one ballot per wave; lane 0 stores the wave's 64-bit done mask
     // (every wave writes its word each step, so no clearing and no atomics; the host
@@ -799,8 +809,20 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
             sample_ic<MODEL>(P, key, y1, v0);
             B.v0[i] = v0;
             cw = ep << kEpisodeShift;
+            // overwrite the early stores of this env with its reset state / obs
 #pragma unroll
-            for (int j = 0; j < NS; ++j) o[j] = y1[j] * H.inv_norm[j];
+            for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
+            if constexpr (NS % 2 == 0) {
+#pragma unroll
+                for (int j = 0; j < NS / 2; ++j)
+                    __builtin_amdgcn_raw_buffer_store_b64(
+                        u32x2{__float_as_uint(y1[2 * j] * H.inv_norm[2 * j]),
+                              __float_as_uint(y1[2 * j + 1] * H.inv_norm[2 * j + 1])},
+                        obs_r, (int)((i * NS + 2 * j) * 4u), 0, 0);
+            } else {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) bst_f(obs_r, y1[j] * H.inv_norm[j], (i * NS + j) * 4u, 0);
+            }
             el = 0;
             ret = 0.0f;
         }
@@ -809,8 +831,6 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     RR_STAMP(5);
 
     if (valid) {
-#pragma unroll
-        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
         if (use_counter) bst_u(cw_r, cw, vo, 0);
         if (P.flags & RR_FLAG_EPISODE_STATS) bst_f(ret_r, ret, vo, 0);
         bst_f(make_rsrc(io.reward, plane), r, vo, 0);
@@ -824,9 +844,6 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
             bst_f(tr, event ? 1.0f : 0.0f, vo, (NT + 1) * plane);  // solve_ivp status == 1
         }
     }
-    const uint32_t nvalid = (n - wave_base) < (uint32_t)EPW ? (n - wave_base) : (uint32_t)EPW;
-    store_obs_tile<NS, EPW>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
-                            io.obs_vec_ok);
     RR_STAMP(6);
 #if RR_DIAG == 4
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
