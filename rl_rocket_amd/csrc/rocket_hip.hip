@@ -516,6 +516,19 @@ __device__ __forceinline__ void sample_ic(const KParams& P, const ResetKey& k, f
     }
 }
 
+// X < r c and X > r c with r = sqrt(X^2 + Y^2) >= 0 (given r2 = r^2), without the sqrt:
+// for c >= 0, X < rc <=> X < 0 or X^2 < c^2 r2; for c < 0, X < rc <=> X < 0 and X^2 > c^2 r2.
+__device__ __forceinline__ bool lt_rc(float X, float r2, float c)
+{
+    const float x2 = X * X, q = (c * c) * r2;
+    return c >= 0.0f ? (X < 0.0f || x2 < q) : (X < 0.0f && x2 > q);
+}
+__device__ __forceinline__ bool gt_rc(float X, float r2, float c)
+{
+    const float x2 = X * X, q = (c * c) * r2;
+    return c >= 0.0f ? (X > 0.0f && x2 > q) : (X >= 0.0f || x2 < q);
+}
+
 // Reward / done of the reference env on the float32 post-step state.
 template <int MODEL>
 __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s, const float* a, float v0,
@@ -538,8 +551,7 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
             tau_inv = 1.0f / 100.0f;
         }
         float nrh = fsqrt(rh0 * rh0 + rh1 * rh1 + rh2 * rh2);
-        float nvh = fsqrt(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
-        float t_go = nrh * frcp(nvh);
+        float t_go = nrh * frsq(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
         float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * one_minus_exp_neg(t_go * tau_inv);
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
         t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1 + e2 * e2);
@@ -555,15 +567,16 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         float R02 = 2.0f * (x * z + y * w);
         float mR12 = 2.0f * (x * w - y * z);
         float R22 = w * w - x * x - y * y + z * z;
-        float ra = fsqrt(R00 * R00 + mR01 * mR01);
-        float rc = fsqrt(R22 * R22 + mR12 * mR12);
-        float sb = fabsf(R02) / qq;
-        bool att = (!(P.att_never & 1u) && R00 < ra * P.att_c[0]) || (!(P.att_never & 2u) && sb > P.att_c[1]) ||
-                   (!(P.att_never & 4u) && R22 < rc * P.att_c[2]);
+        const float ra2 = R00 * R00 + mR01 * mR01;
+        const float rc2 = R22 * R22 + mR12 * mR12;
+        const float sb = fabsf(R02);  // |sin b| * qq
+        bool att = (!(P.att_never & 1u) && lt_rc(R00, ra2, P.att_c[0])) ||
+                   (!(P.att_never & 2u) && sb > P.att_c[1] * qq) ||
+                   (!(P.att_never & 4u) && lt_rc(R22, rc2, P.att_c[2]));
         t[3] = att ? P.gamma : 0.0f;
         // _check_landing (rocket_env.py:1040-1061); any() over angles and omega is the reference's
-        bool att_ok = (P.land_always & 1u) || R00 > ra * P.land_c[0] || (P.land_always & 2u) ||
-                      sb < P.land_c[1] || (P.land_always & 4u) || R22 > rc * P.land_c[2];
+        bool att_ok = (P.land_always & 1u) || gt_rc(R00, ra2, P.land_c[0]) || (P.land_always & 2u) ||
+                      sb < P.land_c[1] * qq || (P.land_always & 4u) || gt_rc(R22, rc2, P.land_c[2]);
         bool om_ok = fabsf(s[10]) < P.omega_lt || fabsf(s[11]) < P.omega_lt || fabsf(s[12]) < P.omega_lt;
         float r2 = s[0] * s[0] + s[1] * s[1] + s[2] * s[2];
         float v2 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
@@ -586,8 +599,7 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
             tau_inv = 1.0f / 100.0f;
         }
         float nrh = fsqrt(rh0 * rh0 + rh1 * rh1);
-        float nvh = fsqrt(s[3] * s[3] + vh1 * vh1);
-        float t_go = nrh * frcp(nvh);
+        float t_go = nrh * frsq(s[3] * s[3] + vh1 * vh1);
         float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * one_minus_exp_neg(t_go * tau_inv);
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1;
         t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1);
