@@ -124,7 +124,7 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
         H.inv_norm[j] = P.inv_norm[j];
-        pin_s(H.inv_norm[j]);
+        asm volatile("" : "+v"(H.inv_norm[j]));
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -132,10 +132,10 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
         H.bhi[j] = P.bhi[j];
         H.att_c[j] = P.att_c[j];
         H.land_c[j] = P.land_c[j];
-        pin_s(H.blo[j]);
-        pin_s(H.bhi[j]);
-        pin_s(H.att_c[j]);
-        pin_s(H.land_c[j]);
+        asm volatile("" : "+v"(H.blo[j]));
+        asm volatile("" : "+v"(H.bhi[j]));
+        asm volatile("" : "+v"(H.att_c[j]));
+        asm volatile("" : "+v"(H.land_c[j]));
     }
 #define RR_HOT(f) \
     H.f = P.f;    \
@@ -516,19 +516,6 @@ __device__ __forceinline__ void sample_ic(const KParams& P, const ResetKey& k, f
     }
 }
 
-// X < r c and X > r c with r = sqrt(X^2 + Y^2) >= 0 (given r2 = r^2), without the sqrt:
-// for c >= 0, X < rc <=> X < 0 or X^2 < c^2 r2; for c < 0, X < rc <=> X < 0 and X^2 > c^2 r2.
-__device__ __forceinline__ bool lt_rc(float X, float r2, float c)
-{
-    const float x2 = X * X, q = (c * c) * r2;
-    return c >= 0.0f ? (X < 0.0f || x2 < q) : (X < 0.0f && x2 > q);
-}
-__device__ __forceinline__ bool gt_rc(float X, float r2, float c)
-{
-    const float x2 = X * X, q = (c * c) * r2;
-    return c >= 0.0f ? (X > 0.0f && x2 > q) : (X >= 0.0f || x2 < q);
-}
-
 // Reward / done of the reference env on the float32 post-step state.
 template <int MODEL>
 __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s, const float* a, float v0,
@@ -567,16 +554,15 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         float R02 = 2.0f * (x * z + y * w);
         float mR12 = 2.0f * (x * w - y * z);
         float R22 = w * w - x * x - y * y + z * z;
-        const float ra2 = R00 * R00 + mR01 * mR01;
-        const float rc2 = R22 * R22 + mR12 * mR12;
-        const float sb = fabsf(R02);  // |sin b| * qq
-        bool att = (!(P.att_never & 1u) && lt_rc(R00, ra2, P.att_c[0])) ||
-                   (!(P.att_never & 2u) && sb > P.att_c[1] * qq) ||
-                   (!(P.att_never & 4u) && lt_rc(R22, rc2, P.att_c[2]));
+        float ra = fsqrt(R00 * R00 + mR01 * mR01);
+        float rc = fsqrt(R22 * R22 + mR12 * mR12);
+        float sb = fabsf(R02) / qq;
+        bool att = (!(P.att_never & 1u) && R00 < ra * P.att_c[0]) || (!(P.att_never & 2u) && sb > P.att_c[1]) ||
+                   (!(P.att_never & 4u) && R22 < rc * P.att_c[2]);
         t[3] = att ? P.gamma : 0.0f;
         // _check_landing (rocket_env.py:1040-1061); any() over angles and omega is the reference's
-        bool att_ok = (P.land_always & 1u) || gt_rc(R00, ra2, P.land_c[0]) || (P.land_always & 2u) ||
-                      sb < P.land_c[1] * qq || (P.land_always & 4u) || gt_rc(R22, rc2, P.land_c[2]);
+        bool att_ok = (P.land_always & 1u) || R00 > ra * P.land_c[0] || (P.land_always & 2u) ||
+                      sb < P.land_c[1] || (P.land_always & 4u) || R22 > rc * P.land_c[2];
         bool om_ok = fabsf(s[10]) < P.omega_lt || fabsf(s[11]) < P.omega_lt || fabsf(s[12]) < P.omega_lt;
         float r2 = s[0] * s[0] + s[1] * s[1] + s[2] * s[2];
         float v2 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
@@ -599,7 +585,8 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
             tau_inv = 1.0f / 100.0f;
         }
         float nrh = fsqrt(rh0 * rh0 + rh1 * rh1);
-        float t_go = nrh * frsq(s[3] * s[3] + vh1 * vh1);
+        float nvh = fsqrt(s[3] * s[3] + vh1 * vh1);
+        float t_go = nrh * frcp(nvh);
         float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * one_minus_exp_neg(t_go * tau_inv);
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1;
         t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1);
@@ -671,14 +658,13 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     const uint32_t vo = ic * 4u;           // per-lane byte offset in every fp32/u32 plane
     const uint32_t plane = n * 4u;         // bytes per plane
     const bool use_counter = P.max_steps > 0 || (P.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
-    const rsrc_t st_r = make_rsrc(B.state, (uint64_t)NS * plane);
+    // state planes, v0, counter and ep_ret are consecutive planes of ONE allocation
+    // (rr_create), so a single descriptor (4 SGPRs) serves them all via soffset
+    const rsrc_t st_r = make_rsrc(B.state, (uint64_t)(NS + 3) * plane);
     const rsrc_t act_r = make_rsrc(io.action, (uint64_t)NA * plane);
-    const rsrc_t v0_r = make_rsrc(B.v0, plane);
-    const rsrc_t cw_r = make_rsrc(B.counter, plane);
-    const rsrc_t ret_r = make_rsrc(B.ep_ret, plane);
+    const uint32_t v0_off = NS * plane, cw_off = (NS + 1) * plane, ret_off = (NS + 2) * plane;
 #if RR_DIAG == 4
     uint64_t stamp_[8];
-    const uint64_t rt0_ = __builtin_amdgcn_s_memrealtime();
 #endif
     RR_STAMP(0);
 
@@ -704,9 +690,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
         a[0] = __uint_as_float(v.x);
         a[1] = __uint_as_float(v.y);
     }
-    float v0 = bld_f(v0_r, vo, 0);
-    uint32_t cw = use_counter ? bld_u(cw_r, vo, 0) : 0u;
-    float ret = (P.flags & RR_FLAG_EPISODE_STATS) ? bld_f(ret_r, vo, 0) : 0.0f;
+    float v0 = bld_f(st_r, vo, v0_off);
+    uint32_t cw = use_counter ? bld_u(st_r, vo, cw_off) : 0u;
+    float ret = (P.flags & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
 #if RR_DIAG == 4
     {  // force every load to land, then stamp
@@ -751,20 +737,6 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
         y1[2] = fmodf(th, kTwoPi);
     }
 
-    // ---- early stores: the post-step state and obs leave now, so their store burst
-    // drains under the reward / done / reset arithmetic below (envs that end this step
-    // are rewritten after their reset, a rare scattered write) ----
-    const uint32_t nvalid = (n - wave_base) < (uint32_t)EPW ? (n - wave_base) : (uint32_t)EPW;
-    const rsrc_t obs_r = make_rsrc(io.obs, (uint64_t)NS * plane);
-    float o[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) o[j] = y1[j] * H.inv_norm[j];
-    if (valid) {
-#pragma unroll
-        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
-    }
-    store_obs_tile<NS, EPW>(lds[wv], o, obs_r, wave_base, lane, nvalid, io.obs_vec_ok);
-
     bool bv;
     float t[NT];
 #if RR_DIAG == 1
@@ -791,6 +763,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     }
     ret += r;
     RR_STAMP(4);
+
+    float o[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) o[j] = y1[j] * H.inv_norm[j];
 
     // Done compaction: one ballot per wave; lane 0 stores the wave's 64-bit done mask
     // (every wave writes its word each step, so no clearing and no atomics; the host
@@ -819,22 +795,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
             const ResetKey key = reset_key(P.seed, P.id_off + i, ep, y1[0], y1[NS - 1]);
             sample_ic<MODEL>(P, key, y1, v0);
-            B.v0[i] = v0;
+            bst_f(st_r, v0, vo, v0_off);
             cw = ep << kEpisodeShift;
-            // overwrite the early stores of this env with its reset state / obs
 #pragma unroll
-            for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
-            if constexpr (NS % 2 == 0) {
-#pragma unroll
-                for (int j = 0; j < NS / 2; ++j)
-                    __builtin_amdgcn_raw_buffer_store_b64(
-                        u32x2{__float_as_uint(y1[2 * j] * H.inv_norm[2 * j]),
-                              __float_as_uint(y1[2 * j + 1] * H.inv_norm[2 * j + 1])},
-                        obs_r, (int)((i * NS + 2 * j) * 4u), 0, 0);
-            } else {
-#pragma unroll
-                for (int j = 0; j < NS; ++j) bst_f(obs_r, y1[j] * H.inv_norm[j], (i * NS + j) * 4u, 0);
-            }
+            for (int j = 0; j < NS; ++j) o[j] = y1[j] * H.inv_norm[j];
             el = 0;
             ret = 0.0f;
         }
@@ -843,8 +807,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     RR_STAMP(5);
 
     if (valid) {
-        if (use_counter) bst_u(cw_r, cw, vo, 0);
-        if (P.flags & RR_FLAG_EPISODE_STATS) bst_f(ret_r, ret, vo, 0);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
+        if (use_counter) bst_u(st_r, cw, vo, cw_off);
+        if (P.flags & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, ret_off);
         bst_f(make_rsrc(io.reward, plane), r, vo, 0);
         bst_u8(make_rsrc(io.done, n), (uint8_t)done, i);
         if (io.truncated) bst_u8(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
@@ -856,16 +822,16 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
             bst_f(tr, event ? 1.0f : 0.0f, vo, (NT + 1) * plane);  // solve_ivp status == 1
         }
     }
+    const uint32_t nvalid = (n - wave_base) < (uint32_t)EPW ? (n - wave_base) : (uint32_t)EPW;
+    store_obs_tile<NS, EPW>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
+                            io.obs_vec_ok);
     RR_STAMP(6);
 #if RR_DIAG == 4
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     RR_STAMP(7);
-    const uint64_t rt1_ = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 10 + k] = stamp_[k];
-        B.stamps[(size_t)wave_idx * 10 + 8] = rt0_;
-        B.stamps[(size_t)wave_idx * 10 + 9] = rt1_;
+        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 8 + k] = stamp_[k];
     }
 #endif
 }
@@ -1073,7 +1039,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     if (p->integrator != RR_INT_RK4 && p->integrator != RR_INT_EULER)
         return fail(RR_EINVAL, "rr_create: unknown integrator");
     const int64_t ns_ = p->model == RR_MODEL_6DOF ? 14 : 7;
-    if (n <= 0 || n * ns_ * 4 > (int64_t)0xFFFFFFFF)
+    if (n <= 0 || n * (ns_ + 3) * 4 > (int64_t)0xFFFFFFFF)
         return fail(RR_EINVAL, "rr_create: n must be >= 1 and n*state_dim*4 must fit 32-bit buffer offsets");
     if (p->max_episode_steps < 0 || p->max_episode_steps > (int32_t)kElapsedMask)
         return fail(RR_EINVAL, "rr_create: max_episode_steps must be in [0, 65535]");
@@ -1093,15 +1059,14 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         void** ptr;
         size_t bytes;
     } allocs[] = {
-        {(void**)&e->state, sizeof(float) * e->ns * n},   {(void**)&e->v0, sizeof(float) * n},
-        {(void**)&e->counter, sizeof(uint32_t) * n},
-        {(void**)&e->ep_ret, sizeof(float) * n},          {(void**)&e->done_bits, sizeof(uint64_t) * n_words(n)},
+        {(void**)&e->state, sizeof(float) * (e->ns + 3) * n},  // + v0, counter, ep_ret planes
+        {(void**)&e->done_bits, sizeof(uint64_t) * n_words(n)},
         {(void**)&e->term_obs, sizeof(float) * e->ns * n},
         {(void**)&e->term_ret, sizeof(float) * n},        {(void**)&e->term_len, sizeof(int32_t) * n},
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
 #if RR_DIAG == 4
-        {(void**)&e->stamps, sizeof(uint64_t) * 10 * n_words(n)},
+        {(void**)&e->stamps, sizeof(uint64_t) * 8 * n_words(n)},
 #endif
     };
     for (auto& a : allocs) {
@@ -1116,6 +1081,9 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
             return hip_fail(err, "rr_create: hipMemset");
         }
     }
+    e->v0 = e->state + (size_t)e->ns * n;
+    e->counter = reinterpret_cast<uint32_t*>(e->state + (size_t)(e->ns + 1) * n);
+    e->ep_ret = e->state + (size_t)(e->ns + 2) * n;
     e->kp.id_off = env_id_offset;
     int rc = rr_seed(e, 42, nullptr);
     if (rc == RR_OK) {
@@ -1134,7 +1102,7 @@ int rr_destroy(rr_env* e)
 {
     if (!e) return RR_OK;
     DeviceGuard g(e->device);
-    void* ptrs[] = {e->state,    e->v0,       e->counter,  e->ep_ret, e->done_bits,
+    void* ptrs[] = {e->state, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -1299,9 +1267,9 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
 // diagnostic build only: copy the per-wave phase stamps of the last step to the host
 int64_t rr_debug_stamps(rr_env* e, uint64_t* host, int64_t cap)
 {
-    const int64_t nw = std::min<int64_t>(cap / 10, n_words(e->n));
+    const int64_t nw = std::min<int64_t>(cap / 8, n_words(e->n));
     hipError_t err = hipDeviceSynchronize();
-    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 10 * nw, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 8 * nw, hipMemcpyDeviceToHost);
     return err == hipSuccess ? nw : hip_fail(err, "rr_debug_stamps");
 }
 #endif
