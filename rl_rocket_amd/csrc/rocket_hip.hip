@@ -38,8 +38,11 @@
 
 namespace {
 
+#ifndef RR_BLOCK
+#define RR_BLOCK 256
+#endif
 constexpr int kWave = 64;
-constexpr int kBlock = 256;
+constexpr int kBlock = RR_BLOCK;  // threads per workgroup (A/B-tested: tools/ab_kernel.py)
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // ---------------------------------------------------------------------------

@@ -31,9 +31,10 @@ def main():
 
     os.makedirs(a.out, exist_ok=True)
     libs = []
-    for k, src in enumerate(a.sources):
+    for k, spec in enumerate(a.sources):
+        src, _, defs = spec.partition("@")  # "file.hip@NAME=VAL,NAME2=VAL2"
         lib = os.path.join(a.out, "ab_%d.so" % k)
-        cmd = b.command(out=lib)
+        cmd = b.command(out=lib, defines=tuple(d for d in defs.split(",") if d))
         cmd[-1] = os.path.abspath(src)
         subprocess.check_call(cmd)
         libs.append(lib)
