@@ -31,7 +31,8 @@
 // Diagnostic ablations (tools/diag_kernel.py only; the product build has RR_DIAG 0):
 //   1 = memory only (no integration / reward arithmetic), 2 = no event / reset branches,
 //   3 = compute only (state synthesised in registers instead of loaded),
-//   4 = product kernel + s_memtime phase stamps per wave (rr_debug_stamps).
+//   4 = product kernel + s_memtime phase stamps per wave (rr_debug_stamps),
+//   5 = no event path, 6 = no in-kernel reset.
 #ifndef RR_DIAG
 #define RR_DIAG 0
 #endif
@@ -717,7 +718,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     const Ctl c = make_ctl<MODEL>(P, a);
     integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
     const float g0 = y0[EV], g1 = y1[EV];
-#if RR_DIAG == 2
+#if RR_DIAG == 2 || RR_DIAG == 5
     const bool event = false;
 #else
     const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
@@ -794,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
             B.term_ret[i] = ret;
             B.term_len[i] = el;
         }
-        if ((P.flags & RR_FLAG_AUTO_RESET) && dv) {
+        if ((P.flags & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
             const ResetKey key = reset_key(P.seed, P.id_off + i, ep, y1[0], y1[NS - 1]);
             sample_ic<MODEL>(P, key, y1, v0);
