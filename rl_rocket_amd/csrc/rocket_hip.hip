@@ -477,10 +477,10 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         s = x0 * frcp(x0 - x1);
         // Newton from the secant guess, kept inside the closed sign bracket [lo, hi]
         // (bisection fallback). A converged iterate sits on a bracket end, so the test is
-        // inclusive. Fixed 5 iterations, branch-free (quadratic convergence from the secant
+        // inclusive. Fixed 3 iterations, branch-free (quadratic convergence from the secant
         // guess; the parity tests cover touchdowns down to |v| ~ 1 m/s).
 #pragma unroll
-        for (int it = 0; it < 5; ++it) {
+        for (int it = 0; it < 3; ++it) {
             const float s2 = s * s, s3 = s2 * s;
             const float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
                             (s3 - s2) * hv1;
@@ -632,8 +632,11 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
         constexpr int NV = EPW * NS / 4;
         const u32x4* src4 = reinterpret_cast<const u32x4*>(lds);
 #pragma unroll
-        for (int k = lane; k < NV; k += kWave)
-            __builtin_amdgcn_raw_buffer_store_b128(src4[k], obs_r, (int)(k * 16u), (int)sbase, 0);
+        for (int q = 0; q < (NV + kWave - 1) / kWave; ++q) {
+            const int k = lane + q * kWave;
+            if (NV % kWave == 0 || k < NV)
+                __builtin_amdgcn_raw_buffer_store_b128(src4[k], obs_r, (int)(k * 16u), (int)sbase, 0);
+        }
     } else {
         const int tot = (int)nvalid * NS;
         for (int k = lane; k < tot; k += kWave) bst_f(obs_r, lds[k], k * 4u, sbase);
