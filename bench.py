@@ -41,7 +41,69 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="step", choices=["step", "rollout"],
+                    help="step: the fused env step (headline); rollout: on-device PPO rollout "
+                         "collection (MlpPolicy 64x64 forward + sample + env step + buffer), BASELINE configs[4]")
+    ap.add_argument("--rollout-steps", type=int, default=16)
     return ap.parse_args()
+
+
+def bench_rollout(args, dev, n, model, kw):
+    """BASELINE configs[4]: N envs driving an on-device PPO rollout; the whole collect()
+    (n_steps x [policy forward, Gaussian sample, env step, timeout bootstrap, buffer
+    writes] + GAE) is one hipGraph; obs never leave HBM."""
+    import torch
+
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import MAX_EPISODE_STEPS
+    from rl_rocket_amd.rollout import DeviceRollout, MlpActorCritic, ppo_update
+
+    torch.manual_seed(42)
+    env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
+                      episode_stats=False, integrator=args.integrator, **kw)
+    pol = MlpActorCritic(env.state_dim, env.action_dim).to(dev)
+    ro = DeviceRollout(env, pol, n_steps=args.rollout_steps)
+    for _ in range(3):
+        ro.collect()
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            ro.collect()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    reps = max(2, args.steps // args.rollout_steps)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    steps = reps * args.rollout_steps
+    opt = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    stats = ppo_update(pol, opt, ro, n_epochs=1, batch_size=n)
+    torch.cuda.synchronize(dev)
+    upd = time.perf_counter() - t1
+    env.close()
+    return {
+        "metric": "env-steps/sec of on-device PPO rollout collection (%s, N=%d per GPU)"
+                  % ("6DOF" if model == 6 else "3DOF", n),
+        "value": n * steps / dt, "unit": "env-steps/s", "n_gpus": 1, "steps": steps, "warmup": 3 * args.rollout_steps,
+        "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32", "data": "synthetic ICs (env_config init_space), actions from a random-init MlpPolicy",
+        "config": {"workload": "Rocket6DOF N=%d, MlpPolicy(64x64 tanh) forward + Gaussian sample + fused step "
+                               "+ timeout bootstrap + rollout buffer + GAE, n_steps=%d per hipGraph"
+                               % (n, args.rollout_steps), "envs_per_gpu": n},
+        "gpu_ms_per_collect": e0.elapsed_time(e1) / reps,
+        "ppo_epoch_ms": upd * 1e3, "ppo_stats": stats,
+    }
 
 
 def cpu_baseline(model, seconds, seed=0):
@@ -132,6 +194,13 @@ def main():
     model = parse_model(args.model)
     kw = ENV_CONFIG_6DOF if model == 6 else {}
     n = args.n
+    if args.mode == "rollout":
+        res = bench_rollout(args, dev, n, model, kw)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
                       episode_stats=False, integrator=args.integrator, env_id_offset=rank * n, **kw)
     env.reset()

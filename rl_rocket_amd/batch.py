@@ -123,12 +123,15 @@ class RocketBatch:
         m = min(int(c), cap)
         return idx[:m], tobs[:m], ret[:m], ln[:m]
 
-    def copy_terminal(self):
-        """Device copies of the per-env terminal buffers (rows valid where done)."""
+    def copy_terminal(self, out=None):
+        """Device copies of the per-env terminal buffers (rows valid where done). `out` =
+        preallocated (obs [N,ns] f32, return [N] f32, len [N] i32), any may be None."""
         t = self.torch
-        tobs = t.empty((self.num_envs, self.state_dim), dtype=t.float32, device=self.device)
-        ret = t.empty((self.num_envs,), dtype=t.float32, device=self.device)
-        ln = t.empty((self.num_envs,), dtype=t.int32, device=self.device)
+        if out is None:
+            out = (t.empty((self.num_envs, self.state_dim), dtype=t.float32, device=self.device),
+                   t.empty((self.num_envs,), dtype=t.float32, device=self.device),
+                   t.empty((self.num_envs,), dtype=t.int32, device=self.device))
+        tobs, ret, ln = out
         _lib.check(self.lib.rr_copy_terminal(self._h, _ptr(tobs), _ptr(ret), _ptr(ln), self._stream()),
                    "rr_copy_terminal")
         return tobs, ret, ln

@@ -78,3 +78,105 @@ def test_vec_env_sb3_semantics():
     assert seen_trunc
     assert np.all(np.abs(obs) < 10)
     env.close()
+
+
+def test_reward_annealing_flag():
+    """RR_FLAG_REWARD_ANNEALING == RewardAnnealing (wrappers.py:72-86) on the kernel's own terms."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+
+    n = 8192
+    b = RocketBatch(n, model=6, device="cuda:0", reward_annealing=True, compute_terms=True, **ENV_CONFIG_6DOF)
+    b.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(5)
+    for _ in range(30):
+        a = torch.rand((n, 3), device="cuda:0", generator=g) * 2 - 1
+        _, rew, _, _ = b.step(a)
+        t = b.terms
+        ref = t[3] + t[4] - 0.004 * (a[:, 2] + 1)
+        torch.testing.assert_close(rew, ref, rtol=1e-6, atol=1e-6)
+    b.close()
+
+
+def test_euler_mode_is_declared_non_parity(golden3):
+    """RR_INT_EULER (BASELINE 'Euler' config) runs and stays close, but is NOT the parity mode."""
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from gpu_util import floored_rel, run_rows
+
+    rk4 = run_rows(3, golden3)
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = len(golden3["group"])
+    b = RocketBatch(n, model=3, device="cuda:0", auto_reset=False, episode_stats=False, integrator="euler")
+    ic = golden3["ic"].astype(np.float32)
+    v0 = np.sqrt((ic[:, 3:5] ** 2).sum(1, dtype=np.float32)).astype(np.float32)
+    b.set_state(torch.from_numpy(golden3["state_in"].astype(np.float32).T.copy()), v0=torch.from_numpy(v0))
+    b.step(torch.from_numpy(golden3["action"].astype(np.float32)))
+    st = b.get_state()[0].cpu().numpy().T
+    e_eu = floored_rel(st, golden3["state_out"], golden3["normalizer"][:7]).max()
+    e_rk = floored_rel(rk4["state_out"], golden3["state_out"], golden3["normalizer"][:7]).max()
+    assert e_rk < 1e-5 < e_eu < 1e-2
+    b.close()
+
+
+def test_vec_env_3dof():
+    from rl_rocket_amd.vec_env import RocketVecEnv
+
+    env = RocketVecEnv(2048, model="3DOF", device="cuda:0", max_episode_steps=800)
+    obs = env.reset()
+    assert obs.shape == (2048, 7)
+    for _ in range(5):
+        obs, rew, done, infos = env.step(np.zeros((2048, 2), np.float32))
+    assert np.isfinite(obs).all() and np.isfinite(rew).all()
+    env.close()
+
+
+def test_device_rollout_and_ppo_update():
+    """On-device rollout (BASELINE configs[4]): buffers stay on the GPU, GAE matches a
+    host recomputation, a PPO epoch runs; the collect loop is graph-capturable."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout, MlpActorCritic, ppo_update
+
+    torch.manual_seed(0)
+    n, T = 4096, 8
+    env = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=20, auto_reset=True, **ENV_CONFIG_6DOF)
+    pol = MlpActorCritic(14, 3).cuda()
+    ro = DeviceRollout(env, pol, n_steps=T)
+    ro.collect()
+    assert ro.obs.is_cuda and ro.obs.shape == (T, n, 14)
+    for t in (ro.obs, ro.actions, ro.rewards, ro.values, ro.log_probs, ro.advantages):
+        assert torch.isfinite(t).all()
+    # GAE on the host from the same tensors
+    r, v, s = ro.rewards.cpu().numpy(), ro.values.cpu().numpy(), ro.starts.cpu().numpy()
+    lv, ld = ro.last_value.cpu().numpy(), ro.last_done.cpu().numpy()
+    adv = np.zeros_like(r)
+    last = np.zeros(n, np.float32)
+    for t in reversed(range(T)):
+        nt = 1.0 - (ld if t == T - 1 else s[t + 1])
+        nv = lv if t == T - 1 else v[t + 1]
+        last = r[t] + 0.99 * nv * nt - v[t] + 0.99 * 0.95 * nt * last
+        adv[t] = last
+    np.testing.assert_allclose(ro.advantages.cpu().numpy(), adv, rtol=1e-4, atol=1e-4)
+    before = [p.detach().clone() for p in pol.parameters()]
+    opt = torch.optim.Adam(pol.parameters(), lr=3e-4)
+    stats = ppo_update(pol, opt, ro, n_epochs=1, batch_size=8192)
+    assert all(np.isfinite(list(stats.values())))
+    assert any(not torch.equal(a, b) for a, b in zip(before, pol.parameters()))
+    # graph capture of one collect
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(g, stream=st):
+            ro.collect()
+    torch.cuda.current_stream().wait_stream(st)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.isfinite(ro.rewards).all()
+    env.close()
