@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 1
+#define RR_ABI_VERSION 2
 
 /* error codes */
 #define RR_OK 0
@@ -54,40 +54,50 @@ extern "C" {
 #define RR_MODEL_3DOF 3
 #define RR_MODEL_6DOF 6
 
-/* integrators. RK4 is the parity mode (matches the reference's adaptive RK45 +
- * terminal ground event to <= 1e-5 floored-relative). EULER is a
- * declared NON-parity speed mode (BASELINE config "3DOF Euler"). */
+/* integrators. RK4 is the fast parity mode (fp32 state; matches the reference's
+ * adaptive RK45 + terminal ground event to <= 1e-5 floored-relative).
+ * EULER is a declared NON-parity speed mode (BASELINE config "3DOF Euler").
+ * DOPRI5 is the exact mode: fp64 state and the reference's own integrator
+ * (scipy RK45: select_initial_step, DOPRI5 tableau, RMS error controller, dense-output
+ * brentq ground event; simulator.py:230-241 / :58-69), per-env adaptive, with the
+ * simulator clock t (round(t + dt, 3), simulator.py:245) kept as elapsed_steps * dt. */
 #define RR_INT_RK4 0
 #define RR_INT_EULER 1
+#define RR_INT_DOPRI5 2
 
 /* rr_params.flags */
 #define RR_FLAG_AUTO_RESET 0x1        /* reset done envs inside rr_step (SB3 vec-env semantics) */
 #define RR_FLAG_EPISODE_STATS 0x2     /* keep per-env episode return (Monitor) */
 #define RR_FLAG_REWARD_ANNEALING 0x4  /* reward = attitude + goal - xi*(a_thrust+1)  (wrappers.py:72-86) */
 #define RR_FLAG_ACTION_SOA 0x8        /* action laid out [n_act][N] instead of [N][n_act] */
+#define RR_FLAG_SCIPY_H0_CLAMP 0x10   /* DOPRI5: scipy >= 1.12 select_initial_step (clamp h0 to
+                                         the interval); default = scipy 1.7 (requirements.txt:73) */
 
 #define RR_MAX_STATE 14
 
 /* Per-config constants. Lowered on the host from the reference env kwargs
- * (rl_rocket_amd/params.py restates rocket_env.py:51-123 / :557-658). */
+ * (rl_rocket_amd/params.py restates rocket_env.py:51-123 / :557-658). Values the
+ * reference holds as Python floats are double here; the fp32 kernels round them once
+ * at rr_create (bounds with the rounding direction that keeps each comparison exact). */
 typedef struct rr_params {
     int32_t model;               /* RR_MODEL_3DOF | RR_MODEL_6DOF */
     int32_t integrator;          /* RR_INT_* */
     int32_t max_episode_steps;   /* gym TimeLimit; 0 = none */
     uint32_t flags;              /* RR_FLAG_* */
-    float dt;                    /* timestep [s] */
+    double dt;                   /* timestep [s] */
     float ic_low[RR_MAX_STATE];  /* init_space Box low  (float32, rocket_env.py:564-567) */
     float ic_high[RR_MAX_STATE]; /* init_space Box high */
-    float normalizer[RR_MAX_STATE]; /* state_normalizer (rocket_env.py:592-612 / :76-94) */
-    float bounds_low[3];         /* 6DOF: position Box low; 3DOF: [-x_bound, -, -] */
-    float bounds_high[3];        /* 6DOF: position Box high; 3DOF: [x_bound, z_bound, -] */
-    float max_gimbal;            /* rad */
-    float max_thrust;            /* N */
-    float alfa, beta, eta, gamma, delta, kappa, xi; /* reward_coeff */
-    float waypoint, landing_radius, max_velocity;
-    float att_limit[3];          /* trajectory_limits["attitude_limit"] (zyx) */
-    float land_att_limit[3];     /* landing_params["landing_attitude_limit"] */
-    float omega_lim[3];          /* 0.2 hard-coded in the reference (rocket_env.py:656) */
+    double normalizer[RR_MAX_STATE]; /* state_normalizer, float64 (rocket_env.py:592-612 / :76-94) */
+    double bounds_low[3];        /* 6DOF: position Box low (float32 values, inclusive);
+                                    3DOF: [-x_bound, -, -] (x <= -x_bound is out) */
+    double bounds_high[3];       /* 6DOF: position Box high; 3DOF: [x_bound, z_bound, -] (>= is out) */
+    double max_gimbal;           /* rad */
+    double max_thrust;           /* N */
+    double alfa, beta, eta, gamma, delta, kappa, xi; /* reward_coeff */
+    double waypoint, landing_radius, max_velocity;
+    double att_limit[3];         /* trajectory_limits["attitude_limit"] (zyx) */
+    double land_att_limit[3];    /* landing_params["landing_attitude_limit"] */
+    double omega_lim[3];         /* 0.2 hard-coded in the reference (rocket_env.py:656) */
 } rr_params;
 
 /* Library-owned device buffers, valid until rr_destroy. done_bits / terminal_* refer
@@ -118,7 +128,7 @@ int rr_state_dim(const rr_env* e);
 int rr_action_dim(const rr_env* e);
 
 /* Set the key of the reset stream. Resets are counter-based: env `gid` starting its
- * episode `e` draws its initial condition from splitmix64/xoshiro128+ keyed on
+ * episode `e` draws its initial condition from a splitmix64 key + 32-bit mixer keyed on
  * (seed, gid, e, bits of the state it replaces) — deterministic, independent of how
  * envs are sharded over GPUs, and free of per-env RNG state in HBM. Host-only call. */
 int rr_seed(rr_env* e, uint64_t seed, void* stream);
@@ -145,6 +155,11 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
  * TimeLimit steps in bits 0-15, episodes started in bits 16-31 (keys the reset stream). */
 int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32_t* elapsed, void* stream);
 int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void* stream);
+/* Same with an fp64 state [state_dim][N]. Under RR_INT_DOPRI5 this is the state the
+ * integrator carries (the reference's float64 SIM.state); otherwise it is converted
+ * to / from the fp32 planes. In DOPRI5 mode elapsed also sets the clock: t = steps*dt. */
+int rr_set_state64(rr_env* e, const double* state_soa, const float* v0, const int32_t* elapsed, void* stream);
+int rr_get_state64(rr_env* e, double* state_soa, float* v0, int32_t* elapsed, void* stream);
 
 /* Pointers to the library-owned buffers (done list of the last step, etc.). */
 int rr_get_buffers(rr_env* e, rr_buffers* out);

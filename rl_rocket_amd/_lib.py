@@ -13,19 +13,21 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
-RR_INT_RK4, RR_INT_EULER = 0, 1
+RR_INT_RK4, RR_INT_EULER, RR_INT_DOPRI5 = 0, 1, 2
 RR_FLAG_AUTO_RESET = 0x1
 RR_FLAG_EPISODE_STATS = 0x2
 RR_FLAG_REWARD_ANNEALING = 0x4
 RR_FLAG_ACTION_SOA = 0x8
+RR_FLAG_SCIPY_H0_CLAMP = 0x10
 RR_MAX_STATE = 14
 
-_f3 = ctypes.c_float * 3
+_d3 = ctypes.c_double * 3
 _f14 = ctypes.c_float * RR_MAX_STATE
+_d14 = ctypes.c_double * RR_MAX_STATE
 
 
 class RrParams(ctypes.Structure):
@@ -36,27 +38,27 @@ class RrParams(ctypes.Structure):
         ("integrator", ctypes.c_int32),
         ("max_episode_steps", ctypes.c_int32),
         ("flags", ctypes.c_uint32),
-        ("dt", ctypes.c_float),
+        ("dt", ctypes.c_double),
         ("ic_low", _f14),
         ("ic_high", _f14),
-        ("normalizer", _f14),
-        ("bounds_low", _f3),
-        ("bounds_high", _f3),
-        ("max_gimbal", ctypes.c_float),
-        ("max_thrust", ctypes.c_float),
-        ("alfa", ctypes.c_float),
-        ("beta", ctypes.c_float),
-        ("eta", ctypes.c_float),
-        ("gamma", ctypes.c_float),
-        ("delta", ctypes.c_float),
-        ("kappa", ctypes.c_float),
-        ("xi", ctypes.c_float),
-        ("waypoint", ctypes.c_float),
-        ("landing_radius", ctypes.c_float),
-        ("max_velocity", ctypes.c_float),
-        ("att_limit", _f3),
-        ("land_att_limit", _f3),
-        ("omega_lim", _f3),
+        ("normalizer", _d14),
+        ("bounds_low", _d3),
+        ("bounds_high", _d3),
+        ("max_gimbal", ctypes.c_double),
+        ("max_thrust", ctypes.c_double),
+        ("alfa", ctypes.c_double),
+        ("beta", ctypes.c_double),
+        ("eta", ctypes.c_double),
+        ("gamma", ctypes.c_double),
+        ("delta", ctypes.c_double),
+        ("kappa", ctypes.c_double),
+        ("xi", ctypes.c_double),
+        ("waypoint", ctypes.c_double),
+        ("landing_radius", ctypes.c_double),
+        ("max_velocity", ctypes.c_double),
+        ("att_limit", _d3),
+        ("land_att_limit", _d3),
+        ("omega_lim", _d3),
     ]
 
 
@@ -91,6 +93,8 @@ SIGNATURES = {
     "rr_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "rr_set_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_get_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "rr_set_state64": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "rr_get_state64": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_get_buffers": (ctypes.c_int, [_P, ctypes.POINTER(RrBuffers)]),
     "rr_fetch_done": (ctypes.c_int64, [_P, ctypes.c_int64, _P, _P, _P, _P, _P]),
     "rr_copy_terminal": (ctypes.c_int, [_P, _P, _P, _P, _P]),

@@ -20,7 +20,7 @@ def _ptr(t):
 class RocketBatch:
     def __init__(self, num_envs, model="6DOF", device=None, max_episode_steps=0, auto_reset=True,
                  episode_stats=True, reward_annealing=False, integrator="rk4", env_id_offset=0,
-                 compute_terms=False, seed=None, **env_kwargs):
+                 compute_terms=False, seed=None, scipy_h0_clamp=False, **env_kwargs):
         import torch
 
         self.torch = torch
@@ -39,7 +39,8 @@ class RocketBatch:
         self.action_dim = self.cfg.action_dim
         self.n_terms = len(self.cfg.term_names)
         self.params = lower(self.cfg, max_episode_steps=max_episode_steps, auto_reset=auto_reset,
-                            episode_stats=episode_stats, reward_annealing=reward_annealing, integrator=integrator)
+                            episode_stats=episode_stats, reward_annealing=reward_annealing, integrator=integrator,
+                            scipy_h0_clamp=scipy_h0_clamp)
         self.lib = _lib.load()
         h = ctypes.c_void_p()
         _lib.check(self.lib.rr_create(ctypes.byref(h), ctypes.byref(self.params), self.num_envs, int(env_id_offset),
@@ -106,6 +107,25 @@ class RocketBatch:
         v = t.empty((self.num_envs,), dtype=t.float32, device=self.device)
         el = t.empty((self.num_envs,), dtype=t.int32, device=self.device)
         _lib.check(self.lib.rr_get_state(self._h, _ptr(st), _ptr(v), _ptr(el), self._stream()), "rr_get_state")
+        return st, v, el
+
+    def set_state64(self, state_soa, v0=None, elapsed=None):
+        """fp64 state [state_dim][N] (the integrator's own state under integrator="dopri5";
+        elapsed also sets the simulator clock t = steps * dt there)."""
+        t = self.torch
+        st = t.as_tensor(state_soa, device=self.device, dtype=t.float64).reshape(self.state_dim, self.num_envs)
+        st = st.contiguous()
+        v = None if v0 is None else t.as_tensor(v0, device=self.device, dtype=t.float32).reshape(-1).contiguous()
+        el = None if elapsed is None else t.as_tensor(elapsed, device=self.device, dtype=t.int32).reshape(-1).contiguous()
+        self._keep = (st, v, el)
+        _lib.check(self.lib.rr_set_state64(self._h, _ptr(st), _ptr(v), _ptr(el), self._stream()), "rr_set_state64")
+
+    def get_state64(self):
+        t = self.torch
+        st = t.empty((self.state_dim, self.num_envs), dtype=t.float64, device=self.device)
+        v = t.empty((self.num_envs,), dtype=t.float32, device=self.device)
+        el = t.empty((self.num_envs,), dtype=t.int32, device=self.device)
+        _lib.check(self.lib.rr_get_state64(self._h, _ptr(st), _ptr(v), _ptr(el), self._stream()), "rr_get_state64")
         return st, v, el
 
     def fetch_done(self, capacity=None):

@@ -10,6 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "rocket_hip.hip")
+DEPS = [os.path.join(HERE, "csrc", "rocket_dopri5.inc")]
 HEADER = os.path.join(ROOT, "include", "rocket_hip.h")
 OUT = os.path.join(HERE, "librocket_hip.so")
 ARCH = os.environ.get("RR_OFFLOAD_ARCH", "gfx950")
@@ -36,7 +37,7 @@ def up_to_date():
     if not os.path.exists(OUT):
         return False
     t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(p) <= t for p in (SRC, HEADER, __file__))
+    return all(os.path.getmtime(p) <= t for p in [SRC, HEADER, __file__] + DEPS)
 
 
 def build(force=False, resource_usage=False, verbose=True):

@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
 
 template <int MODEL>
 __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bufs B, const uint8_t* mask,
-                                                      float* obs)
+                                                      float* obs, double* state64)
 {
     constexpr int NS = Dims<MODEL>::NS;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -858,6 +858,10 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
         sample_ic<MODEL>(P, key, s, v0);
 #pragma unroll
         for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = s[j];
+        if (state64) {  // RR_INT_DOPRI5
+#pragma unroll
+            for (int j = 0; j < NS; ++j) state64[(int64_t)j * n + i] = (double)s[j];
+        }
         B.v0[i] = v0;
         B.counter[i] = ep << kEpisodeShift;
         B.ep_ret[i] = 0.0f;
@@ -884,6 +888,12 @@ __global__ __launch_bounds__(kBlock) void gather_done_kernel(const int32_t* idx,
     g_ret[k] = term_ret[i];
     g_len[k] = term_len[i];
 }
+
+// Exact-integrator mode (RR_INT_DOPRI5): fp64 scipy RK45 restatement, compiled without
+// FMA contraction so its roundings follow the reference's numpy arithmetic.
+#pragma clang fp contract(off)
+#include "rocket_dopri5.inc"
+#pragma clang fp contract(fast)
 
 // ---------------------------------------------------------------------------
 // Host side
@@ -921,28 +931,34 @@ KParams make_kparams(const rr_params& p)
     const int ns = p.model == RR_MODEL_6DOF ? 14 : 7;
     k.max_steps = p.max_episode_steps;
     k.flags = p.flags;
-    k.h = p.dt;
-    k.h2 = 0.5f * p.dt;
-    k.h6 = p.dt / 6.0f;
+    k.h = (float)p.dt;
+    k.h2 = 0.5f * k.h;
+    k.h6 = k.h / 6.0f;
     for (int j = 0; j < ns; ++j) {
         k.ic_low[j] = p.ic_low[j];
         k.ic_span[j] = p.ic_high[j] - p.ic_low[j];
-        k.inv_norm[j] = (float)(1.0 / (double)p.normalizer[j]);
+        k.inv_norm[j] = (float)(1.0 / p.normalizer[j]);
     }
+    // fp32 thresholds equivalent to the reference's float64 comparisons of float32 values
     for (int j = 0; j < 3; ++j) {
-        k.blo[j] = p.bounds_low[j];
-        k.bhi[j] = p.bounds_high[j];
+        if (p.model == RR_MODEL_6DOF) {  // inside <=> lo <= x <= hi
+            k.blo[j] = ceil_f(p.bounds_low[j]);
+            k.bhi[j] = floor_f(p.bounds_high[j]);
+        } else {                         // out <=> x <= lo | x >= hi
+            k.blo[j] = floor_f(p.bounds_low[j]);
+            k.bhi[j] = ceil_f(p.bounds_high[j]);
+        }
     }
-    k.max_gimbal = p.max_gimbal;
-    k.half_thrust = 0.5f * p.max_thrust;
-    k.alfa = p.alfa;
-    k.beta = p.beta;
-    k.eta = p.eta;
-    k.gamma = p.gamma;
-    k.delta = p.delta;
-    k.kappa = p.kappa;
-    k.xi = p.xi;
-    k.waypoint = p.waypoint;
+    k.max_gimbal = (float)p.max_gimbal;
+    k.half_thrust = (float)(0.5 * p.max_thrust);
+    k.alfa = (float)p.alfa;
+    k.beta = (float)p.beta;
+    k.eta = (float)p.eta;
+    k.gamma = (float)p.gamma;
+    k.delta = (float)p.delta;
+    k.kappa = (float)p.kappa;
+    k.xi = (float)p.xi;
+    k.waypoint = (float)p.waypoint;
     k.land_r2 = (float)((double)p.landing_radius * p.landing_radius);
     k.land_v2 = (float)((double)p.max_velocity * p.max_velocity);
     const double pi = 3.14159265358979323846;
@@ -960,11 +976,42 @@ KParams make_kparams(const rr_params& p)
             else k.land_c[ax] = (float)std::cos(M);
         }
     }
-    k.omega_lt = ceil_f((double)p.omega_lim[0]);
+    k.omega_lt = ceil_f(p.omega_lim[0]);
     k.zero_h = floor_f(1e-3);
     k.seed = 42;
     k.id_off = 0;
     return k;
+}
+
+XParams make_xparams(const rr_params& p)
+{
+    XParams x;
+    std::memset(&x, 0, sizeof(x));
+    x.dt = p.dt;
+    const double ms = std::rint(p.dt * 1000.0);
+    x.dt_milli = (ms > 0 && std::fabs(p.dt * 1000.0 - ms) < 1e-6) ? ms : 0.0;
+    for (int j = 0; j < RR_MAX_STATE; ++j) x.norm[j] = p.normalizer[j];
+    for (int j = 0; j < 3; ++j) {
+        x.lo[j] = p.bounds_low[j];
+        x.hi[j] = p.bounds_high[j];
+        x.att_limit[j] = p.att_limit[j];
+        x.land_att_limit[j] = p.land_att_limit[j];
+        x.omega_lim[j] = p.omega_lim[j];
+    }
+    x.max_gimbal = p.max_gimbal;
+    x.max_thrust = p.max_thrust;
+    x.alfa = p.alfa;
+    x.beta = p.beta;
+    x.eta = p.eta;
+    x.gamma = p.gamma;
+    x.delta = p.delta;
+    x.kappa = p.kappa;
+    x.xi = p.xi;
+    x.waypoint = p.waypoint;
+    x.landing_radius = p.landing_radius;
+    x.max_velocity = p.max_velocity;
+    x.clamp_h0 = (p.flags & RR_FLAG_SCIPY_H0_CLAMP) ? 1 : 0;
+    return x;
 }
 
 }  // namespace
@@ -973,6 +1020,7 @@ struct rr_env {
     int device;
     rr_params p;
     KParams kp;
+    XParams xp;
     int ns, na, nt;
     int64_t n, id_off;
     uint64_t steps;
@@ -984,6 +1032,7 @@ struct rr_env {
     float* term_obs;
     float* term_ret;
     int32_t* term_len;
+    double* state64;    // RR_INT_DOPRI5 only
 #if RR_DIAG == 4
     uint64_t* stamps;
 #endif
@@ -1043,19 +1092,20 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     *out = nullptr;
     if (p->model != RR_MODEL_6DOF && p->model != RR_MODEL_3DOF)
         return fail(RR_EINVAL, "rr_create: model must be 3 or 6");
-    if (p->integrator != RR_INT_RK4 && p->integrator != RR_INT_EULER)
+    if (p->integrator != RR_INT_RK4 && p->integrator != RR_INT_EULER && p->integrator != RR_INT_DOPRI5)
         return fail(RR_EINVAL, "rr_create: unknown integrator");
     const int64_t ns_ = p->model == RR_MODEL_6DOF ? 14 : 7;
     if (n <= 0 || n * (ns_ + 3) * 4 > (int64_t)0xFFFFFFFF)
         return fail(RR_EINVAL, "rr_create: n must be >= 1 and n*state_dim*4 must fit 32-bit buffer offsets");
     if (p->max_episode_steps < 0 || p->max_episode_steps > (int32_t)kElapsedMask)
         return fail(RR_EINVAL, "rr_create: max_episode_steps must be in [0, 65535]");
-    if (!(p->dt > 0.0f)) return fail(RR_EINVAL, "rr_create: dt must be > 0");
+    if (!(p->dt > 0.0)) return fail(RR_EINVAL, "rr_create: dt must be > 0");
     rr_env* e = new (std::nothrow) rr_env();
     if (!e) return fail(RR_ENOMEM, "rr_create: host allocation failed");
     e->device = device;
     e->p = *p;
     e->kp = make_kparams(*p);
+    e->xp = make_xparams(*p);
     e->ns = p->model == RR_MODEL_6DOF ? 14 : 7;
     e->na = p->model == RR_MODEL_6DOF ? 3 : 2;
     e->nt = p->model == RR_MODEL_6DOF ? 5 : 6;
@@ -1076,6 +1126,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->stamps, sizeof(uint64_t) * 8 * n_words(n)},
 #endif
     };
+    const bool exact = p->integrator == RR_INT_DOPRI5;
     for (auto& a : allocs) {
         hipError_t err = hipMalloc(a.ptr, a.bytes);
         if (err != hipSuccess) {
@@ -1086,6 +1137,15 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         if (err != hipSuccess) {
             rr_destroy(e);
             return hip_fail(err, "rr_create: hipMemset");
+        }
+    }
+    if (exact) {
+        const size_t bytes = sizeof(double) * e->ns * n;
+        hipError_t err = hipMalloc((void**)&e->state64, bytes);
+        if (err == hipSuccess) err = hipMemset(e->state64, 0, bytes);
+        if (err != hipSuccess) {
+            rr_destroy(e);
+            return hip_fail(err, "rr_create: hipMalloc (fp64 state)");
         }
     }
     e->v0 = e->state + (size_t)e->ns * n;
@@ -1109,7 +1169,7 @@ int rr_destroy(rr_env* e)
 {
     if (!e) return RR_OK;
     DeviceGuard g(e->device);
-    void* ptrs[] = {e->state, e->done_bits,
+    void* ptrs[] = {e->state, e->state64, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -1135,10 +1195,10 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
     const Bufs b = bufs_of(e);
     if (e->p.model == RR_MODEL_6DOF)
         hipLaunchKernelGGL(reset_kernel<6>, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->kp, b,
-                           mask, obs);
+                           mask, obs, e->state64);
     else
         hipLaunchKernelGGL(reset_kernel<3>, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->kp, b,
-                           mask, obs);
+                           mask, obs, e->state64);
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_reset: launch");
 }
@@ -1161,7 +1221,10 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
     const bool m6 = e->p.model == RR_MODEL_6DOF;
     const bool euler = e->p.integrator == RR_INT_EULER;
     const dim3 grid(grid_of(e->n)), block(kBlock);
-    if (m6 && !euler) hipLaunchKernelGGL((step_kernel<6, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
+    if (e->p.integrator == RR_INT_DOPRI5) {
+        if (m6) hipLaunchKernelGGL(step_exact_kernel<6>, grid, block, 0, s, e->kp, e->xp, b, io, e->state64);
+        else hipLaunchKernelGGL(step_exact_kernel<3>, grid, block, 0, s, e->kp, e->xp, b, io, e->state64);
+    } else if (m6 && !euler) hipLaunchKernelGGL((step_kernel<6, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
     else if (m6) hipLaunchKernelGGL((step_kernel<6, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
     else if (!euler) hipLaunchKernelGGL((step_kernel<3, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
     else hipLaunchKernelGGL((step_kernel<3, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
@@ -1171,18 +1234,52 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
     return RR_OK;
 }
 
-int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32_t* elapsed, void* stream)
+namespace {
+
+// v0 / counter / episode-return part shared by the fp32 and fp64 setters
+hipError_t set_aux(rr_env* e, const float* v0, const int32_t* elapsed, hipStream_t s)
 {
-    if (!e || !state_soa) return fail(RR_EINVAL, "rr_set_state: null argument");
-    hipStream_t s = (hipStream_t)stream;
-    hipError_t err = hipMemcpyAsync(e->state, state_soa, sizeof(float) * e->ns * e->n, hipMemcpyDeviceToDevice, s);
-    if (err == hipSuccess && v0)
-        err = hipMemcpyAsync(e->v0, v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    hipError_t err = hipSuccess;
+    if (v0) err = hipMemcpyAsync(e->v0, v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
     if (err == hipSuccess) {
         if (elapsed) err = hipMemcpyAsync(e->counter, elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
         else err = hipMemsetAsync(e->counter, 0, sizeof(int32_t) * e->n, s);
     }
     if (err == hipSuccess) err = hipMemsetAsync(e->ep_ret, 0, sizeof(float) * e->n, s);
+    return err;
+}
+
+hipError_t get_aux(rr_env* e, float* v0, int32_t* elapsed, hipStream_t s)
+{
+    hipError_t err = hipSuccess;
+    if (v0) err = hipMemcpyAsync(v0, e->v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && elapsed)
+        err = hipMemcpyAsync(elapsed, e->counter, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    return err;
+}
+
+hipError_t widen_async(const float* src, double* dst, int64_t count, hipStream_t s)
+{
+    hipLaunchKernelGGL(widen_kernel, dim3(grid_of(count)), dim3(kBlock), 0, s, src, dst, count);
+    return hipGetLastError();
+}
+
+hipError_t narrow_async(const double* src, float* dst, int64_t count, hipStream_t s)
+{
+    hipLaunchKernelGGL(narrow_kernel, dim3(grid_of(count)), dim3(kBlock), 0, s, src, dst, count);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32_t* elapsed, void* stream)
+{
+    if (!e || !state_soa) return fail(RR_EINVAL, "rr_set_state: null argument");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t cnt = (int64_t)e->ns * e->n;
+    hipError_t err = hipMemcpyAsync(e->state, state_soa, sizeof(float) * cnt, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && e->state64) err = widen_async(e->state, e->state64, cnt, s);
+    if (err == hipSuccess) err = set_aux(e, v0, elapsed, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_set_state");
 }
 
@@ -1193,10 +1290,40 @@ int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void*
     hipError_t err = hipSuccess;
     if (state_soa)
         err = hipMemcpyAsync(state_soa, e->state, sizeof(float) * e->ns * e->n, hipMemcpyDeviceToDevice, s);
-    if (err == hipSuccess && v0) err = hipMemcpyAsync(v0, e->v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
-    if (err == hipSuccess && elapsed)
-        err = hipMemcpyAsync(elapsed, e->counter, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess) err = get_aux(e, v0, elapsed, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_get_state");
+}
+
+int rr_set_state64(rr_env* e, const double* state_soa, const float* v0, const int32_t* elapsed, void* stream)
+{
+    if (!e || !state_soa) return fail(RR_EINVAL, "rr_set_state64: null argument");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t cnt = (int64_t)e->ns * e->n;
+    hipError_t err = hipSuccess;
+    if (e->state64) {
+        err = hipMemcpyAsync(e->state64, state_soa, sizeof(double) * cnt, hipMemcpyDeviceToDevice, s);
+        if (err == hipSuccess) err = narrow_async(e->state64, e->state, cnt, s);
+    } else {
+        err = narrow_async(state_soa, e->state, cnt, s);
+    }
+    if (err == hipSuccess) err = set_aux(e, v0, elapsed, s);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_set_state64");
+}
+
+int rr_get_state64(rr_env* e, double* state_soa, float* v0, int32_t* elapsed, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_get_state64: null handle");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t cnt = (int64_t)e->ns * e->n;
+    hipError_t err = hipSuccess;
+    if (state_soa) {
+        if (e->state64)
+            err = hipMemcpyAsync(state_soa, e->state64, sizeof(double) * cnt, hipMemcpyDeviceToDevice, s);
+        else
+            err = widen_async(e->state, state_soa, cnt, s);
+    }
+    if (err == hipSuccess) err = get_aux(e, v0, elapsed, s);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_get_state64");
 }
 
 int rr_get_buffers(rr_env* e, rr_buffers* out)

@@ -7,9 +7,10 @@ and keeps the same keyword names, defaults and required keys, so that
 ``gym.make("my_environment/Falcon6DOF-v0", **env_config)`` style kwargs
 (configuration_file.py:4-34) work unchanged.
 
-Thresholds that the reference compares in float64 against float32 state values
-are rounded to the float32 value that gives the same answer for every float32
-input (``ceil_f``/``floor_f``), so the kernel can compare in fp32 exactly.
+``rr_params`` carries the reference's float64 values; the fp32 kernels round the
+thresholds that the reference compares in float64 against float32 state values to the
+float32 value that gives the same answer for every float32 input (``ceil_f``/``floor_f``,
+restated in C++ in make_kparams), so they compare in fp32 exactly.
 """
 import copy
 import math
@@ -180,12 +181,17 @@ def parse_model(model):
     raise ValueError("unknown model %r (expected '6DOF' or '3DOF')" % (model,))
 
 
+INTEGRATORS = {"rk4": _lib.RR_INT_RK4, "euler": _lib.RR_INT_EULER, "dopri5": _lib.RR_INT_DOPRI5}
+
+
 def lower(cfg, max_episode_steps=0, auto_reset=True, episode_stats=True, reward_annealing=False,
-          integrator="rk4", action_soa=False, xi_default=0.01):
-    """EnvConfig -> ctypes rr_params."""
+          integrator="rk4", action_soa=False, xi_default=0.01, scipy_h0_clamp=False):
+    """EnvConfig -> ctypes rr_params. ``integrator``: "rk4" (fast parity mode), "euler"
+    (non-parity speed mode) or "dopri5" (exact mode: fp64 scipy RK45 restatement);
+    ``scipy_h0_clamp`` selects scipy >= 1.12's select_initial_step in dopri5 mode."""
     p = _lib.RrParams()
     p.model = cfg.model
-    p.integrator = {"rk4": _lib.RR_INT_RK4, "euler": _lib.RR_INT_EULER}[integrator.lower()]
+    p.integrator = INTEGRATORS[integrator.lower()]
     p.max_episode_steps = int(max_episode_steps or 0)
     flags = 0
     if auto_reset:
@@ -196,6 +202,8 @@ def lower(cfg, max_episode_steps=0, auto_reset=True, episode_stats=True, reward_
         flags |= _lib.RR_FLAG_REWARD_ANNEALING
     if action_soa:
         flags |= _lib.RR_FLAG_ACTION_SOA
+    if scipy_h0_clamp:
+        flags |= _lib.RR_FLAG_SCIPY_H0_CLAMP
     p.flags = flags
     p.dt = float(cfg.kwargs["timestep"])
     ns = cfg.state_dim
@@ -221,10 +229,11 @@ def lower(cfg, max_episode_steps=0, auto_reset=True, episode_stats=True, reward_
         p.landing_radius = float(e["landing_radius"])
         p.max_velocity = float(e["maximum_velocity"])
     else:
-        # _check_bounds: x <= -xb or x >= xb or z >= zb (rocket_env.py:441-445)
-        p.bounds_low[0] = floor_f(-e["x_bound"])
-        p.bounds_high[0] = ceil_f(e["x_bound"])
-        p.bounds_high[1] = ceil_f(e["z_bound"])
+        # _check_bounds: x <= -xb or x >= xb or z >= zb (rocket_env.py:441-445); the fp32
+        # kernels round these with floor_f / ceil_f at rr_create
+        p.bounds_low[0] = -float(e["x_bound"])
+        p.bounds_high[0] = float(e["x_bound"])
+        p.bounds_high[1] = float(e["z_bound"])
         p.waypoint = float(e["waypoint"])
         p.landing_radius = float(e["landing_radius"])
         p.max_velocity = 15.0  # v_lim, rocket_env.py:462

@@ -15,7 +15,7 @@ HEADER = _lib.HEADER
 def _declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(rr_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(rr_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_declares_the_bound_symbols():
@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
     out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH]).decode()
-    exported = set(re.findall(r"\bT (rr_[a-z_]+)", out))
+    exported = set(re.findall(r"\bT (rr_[a-z0-9_]+)", out))
     assert exported == set(_declared_functions())
     assert lib.rr_abi_version() == _lib.ABI_VERSION
 
