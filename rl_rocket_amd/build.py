@@ -26,8 +26,10 @@ def hipcc():
 def command(resource_usage=False, out=OUT, defines=()):
     # -fno-slp-vectorize: the SLP pass packs scalar f32 math into v_pk_* pairs and adds ~180
     # register moves to the step kernel (measured on the .s); the scalar stream is shorter.
+    # kernarg preload: the step kernel's leading pointer / word arguments arrive in user SGPRs
     cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-fno-slp-vectorize", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include")] + ["-D%s" % d for d in defines] + ["-o", out, SRC]
+           "-mllvm", "-amdgpu-kernarg-preload-count=4",
+           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")] + ["-D%s" % d for d in defines] + ["-o", out, SRC]
     if resource_usage:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     return cmd

@@ -75,6 +75,8 @@ constexpr float kTwoPi = 6.28318530717958648f;
 // high 16 bits (keys the counter-based reset stream).
 constexpr uint32_t kElapsedMask = 0xFFFFu;
 constexpr int kEpisodeShift = 16;
+// step_kernel `mode` word: rr_params.flags plus "the counter word is live"
+constexpr uint32_t kModeCounter = 0x80000000u;
 
 // Device-side constants, derived once on the host from rr_params (see make_kparams).
 struct KParams {
@@ -648,14 +650,20 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
 // wave-uniform soffsets (NS*N*4 < 4 GiB, checked at rr_create).
 // EPW = envs per wave (one env per lane). 32 envs per wave (half-empty waves, two per
 // SIMD at N = 65536) was measured slower at every N (tools/diag_kernel.py).
+// The leading four arguments are plain pointers / words so that the command processor
+// preloads them into user SGPRs at wave launch (-mllvm -amdgpu-kernarg-preload-count,
+// rl_rocket_amd/build.py): the first state loads then issue without waiting for scalar
+// loads of the kernarg segment. `mode` = rr_params.flags | kModeCounter.
 template <int MODEL, int INTEG, int EPW = kWave>
-__global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Bufs B, const StepIO io)
+__global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state, const float* __restrict__ action,
+                                                      uint32_t n_envs, uint32_t mode, const KParams P, const Bufs B,
+                                                      const StepIO io)
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][EPW * NS];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = threadIdx.x / kWave;
-    const uint32_t n = (uint32_t)B.n;
+    const uint32_t n = n_envs;
     const uint32_t wave_idx = blockIdx.x * kWavesPerBlock + wv;
     const uint32_t wave_base = wave_idx * EPW;
     if (wave_base >= n) return;  // wave-uniform
@@ -664,11 +672,11 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     const uint32_t ic = valid ? i : n - 1;
     const uint32_t vo = ic * 4u;           // per-lane byte offset in every fp32/u32 plane
     const uint32_t plane = n * 4u;         // bytes per plane
-    const bool use_counter = P.max_steps > 0 || (P.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
+    const bool use_counter = mode & kModeCounter;
     // state planes, v0, counter and ep_ret are consecutive planes of ONE allocation
     // (rr_create), so a single descriptor (4 SGPRs) serves them all via soffset
-    const rsrc_t st_r = make_rsrc(B.state, (uint64_t)(NS + 3) * plane);
-    const rsrc_t act_r = make_rsrc(io.action, (uint64_t)NA * plane);
+    const rsrc_t st_r = make_rsrc(state, (uint64_t)(NS + 3) * plane);
+    const rsrc_t act_r = make_rsrc(action, (uint64_t)NA * plane);
     const uint32_t v0_off = NS * plane, cw_off = (NS + 1) * plane, ret_off = (NS + 2) * plane;
 #if RR_DIAG == 4
     uint64_t stamp_[8];
@@ -684,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
 #pragma unroll
     for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
 #endif
-    if (P.flags & RR_FLAG_ACTION_SOA) {
+    if (mode & RR_FLAG_ACTION_SOA) {
 #pragma unroll
         for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
     } else if constexpr (NA == 3) {
@@ -699,7 +707,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
     }
     float v0 = bld_f(st_r, vo, v0_off);
     uint32_t cw = use_counter ? bld_u(st_r, vo, cw_off) : 0u;
-    float ret = (P.flags & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
+    float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
 #if RR_DIAG == 4
     {  // force every load to land, then stamp
@@ -798,7 +806,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
             B.term_ret[i] = ret;
             B.term_len[i] = el;
         }
-        if ((P.flags & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
+        if ((mode & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
             const ResetKey key = reset_key(P.seed, P.id_off + i, ep, y1[0], y1[NS - 1]);
             sample_ic<MODEL>(P, key, y1, v0);
@@ -817,7 +825,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const KParams P, const Buf
 #pragma unroll
         for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
         if (use_counter) bst_u(st_r, cw, vo, cw_off);
-        if (P.flags & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, ret_off);
+        if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, ret_off);
         bst_f(make_rsrc(io.reward, plane), r, vo, 0);
         bst_u8(make_rsrc(io.done, n), (uint8_t)done, i);
         if (io.truncated) bst_u8(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
@@ -1224,10 +1232,21 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
     if (e->p.integrator == RR_INT_DOPRI5) {
         if (m6) hipLaunchKernelGGL(step_exact_kernel<6>, grid, block, 0, s, e->kp, e->xp, b, io, e->state64);
         else hipLaunchKernelGGL(step_exact_kernel<3>, grid, block, 0, s, e->kp, e->xp, b, io, e->state64);
-    } else if (m6 && !euler) hipLaunchKernelGGL((step_kernel<6, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
-    else if (m6) hipLaunchKernelGGL((step_kernel<6, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
-    else if (!euler) hipLaunchKernelGGL((step_kernel<3, RR_INT_RK4>), grid, block, 0, s, e->kp, b, io);
-    else hipLaunchKernelGGL((step_kernel<3, RR_INT_EULER>), grid, block, 0, s, e->kp, b, io);
+    } else {
+        const uint32_t nn = (uint32_t)e->n;
+        const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
+        const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
+        if (m6 && !euler)
+            hipLaunchKernelGGL((step_kernel<6, RR_INT_RK4>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b, io);
+        else if (m6)
+            hipLaunchKernelGGL((step_kernel<6, RR_INT_EULER>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b,
+                               io);
+        else if (!euler)
+            hipLaunchKernelGGL((step_kernel<3, RR_INT_RK4>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b, io);
+        else
+            hipLaunchKernelGGL((step_kernel<3, RR_INT_EULER>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b,
+                               io);
+    }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return hip_fail(err, "rr_step: launch");
     e->steps++;
