@@ -39,6 +39,21 @@
 
 namespace {
 
+// Cache-policy bits of the step kernel's buffer loads / stores (gfx950 CPol: 1 = sc0,
+// 2 = nt, 16 = sc1); 0 = default policy. RR_ST_AUX: library state planes; RR_OUT_AUX:
+// caller-owned outputs.
+#ifndef RR_LD_AUX
+#define RR_LD_AUX 0
+#endif
+#ifndef RR_ST_AUX
+#define RR_ST_AUX 0
+#endif
+#ifndef RR_OUT_AUX  // caller-owned outputs (obs, reward, done, truncated)
+// sc1 = device-scope write-through: the outputs leave L2 while the kernel runs instead of
+// in the end-of-kernel writeback (A/B at N = 65536: 5.49 -> 5.18 us; the same bit on the
+// state planes, which the next launch re-reads, is slower; nt loads +5 %).
+#define RR_OUT_AUX 16
+#endif
 #ifndef RR_BLOCK
 #define RR_BLOCK 256
 #endif
@@ -221,23 +236,26 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint64_t bytes)
 }
 __device__ __forceinline__ float bld_f(rsrc_t r, uint32_t voff, uint32_t soff)
 {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, RR_LD_AUX));
 }
 __device__ __forceinline__ uint32_t bld_u(rsrc_t r, uint32_t voff, uint32_t soff)
 {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, RR_LD_AUX);
 }
+template <int AUX = RR_ST_AUX>
 __device__ __forceinline__ void bst_f(rsrc_t r, float v, uint32_t voff, uint32_t soff)
 {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)soff, AUX);
 }
+template <int AUX = RR_ST_AUX>
 __device__ __forceinline__ void bst_u(rsrc_t r, uint32_t v, uint32_t voff, uint32_t soff)
 {
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, AUX);
 }
+template <int AUX = RR_ST_AUX>
 __device__ __forceinline__ void bst_u8(rsrc_t r, uint8_t v, uint32_t voff)
 {
-    __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)voff, 0, AUX);
 }
 
 // Element idx of a wave-uniform base pointer with a 32-bit byte offset: lowers to the
@@ -637,11 +655,11 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
         for (int q = 0; q < (NV + kWave - 1) / kWave; ++q) {
             const int k = lane + q * kWave;
             if (NV % kWave == 0 || k < NV)
-                __builtin_amdgcn_raw_buffer_store_b128(src4[k], obs_r, (int)(k * 16u), (int)sbase, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(src4[k], obs_r, (int)(k * 16u), (int)sbase, RR_OUT_AUX);
         }
     } else {
         const int tot = (int)nvalid * NS;
-        for (int k = lane; k < tot; k += kWave) bst_f(obs_r, lds[k], k * 4u, sbase);
+        for (int k = lane; k < tot; k += kWave) bst_f<RR_OUT_AUX>(obs_r, lds[k], k * 4u, sbase);
     }
 }
 
@@ -696,12 +714,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
 #pragma unroll
         for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
     } else if constexpr (NA == 3) {
-        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)(ic * 12u), 0, 0);
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)(ic * 12u), 0, RR_LD_AUX);
         a[0] = __uint_as_float(v.x);
         a[1] = __uint_as_float(v.y);
         a[2] = __uint_as_float(v.z);
     } else {
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(ic * 8u), 0, 0);
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(ic * 8u), 0, RR_LD_AUX);
         a[0] = __uint_as_float(v.x);
         a[1] = __uint_as_float(v.y);
     }
@@ -826,9 +844,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
         for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
         if (use_counter) bst_u(st_r, cw, vo, cw_off);
         if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, ret_off);
-        bst_f(make_rsrc(io.reward, plane), r, vo, 0);
-        bst_u8(make_rsrc(io.done, n), (uint8_t)done, i);
-        if (io.truncated) bst_u8(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
+        bst_f<RR_OUT_AUX>(make_rsrc(io.reward, plane), r, vo, 0);
+        bst_u8<RR_OUT_AUX>(make_rsrc(io.done, n), (uint8_t)done, i);
+        if (io.truncated) bst_u8<RR_OUT_AUX>(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
         if (io.terms) {
             const rsrc_t tr = make_rsrc(io.terms, (uint64_t)(NT + 2) * plane);
 #pragma unroll
