@@ -32,7 +32,7 @@
 //   1 = memory only (no integration / reward arithmetic), 2 = no event / reset branches,
 //   3 = compute only (state synthesised in registers instead of loaded),
 //   4 = product kernel + s_memtime phase stamps per wave (rr_debug_stamps),
-//   5 = no event path, 6 = no in-kernel reset.
+//   5 = no event path, 6 = no in-kernel reset, 7 = empty kernel (launch + dispatch floor).
 #ifndef RR_DIAG
 #define RR_DIAG 0
 #endif
@@ -42,6 +42,12 @@ namespace {
 // Cache-policy bits of the step kernel's buffer loads / stores (gfx950 CPol: 1 = sc0,
 // 2 = nt, 16 = sc1); 0 = default policy. RR_ST_AUX: library state planes; RR_OUT_AUX:
 // caller-owned outputs.
+#ifndef RR_RK4_GENERIC  // 1 = generic 14-component RK4 for 6DOF too (A/B reference)
+#define RR_RK4_GENERIC 0
+#endif
+#ifndef RR_NEWTON_ITERS
+#define RR_NEWTON_ITERS 3
+#endif
 #ifndef RR_LD_AUX
 #define RR_LD_AUX 0
 #endif
@@ -113,7 +119,7 @@ struct KParams {
     uint32_t land_always;     // bit k: "|e_k| < limit" always holds
     float omega_lt;           // |w| < omega_lim  (float threshold, reference 0.2)
     float zero_h;             // x <= 1e-3 as a float threshold
-    uint64_t seed;            // reset stream key (rr_seed)
+    uint32_t seed_w[4];       // reset stream key words (rr_seed)
     int64_t id_off;           // global id of env 0 (multi-GPU shards)
 };
 
@@ -284,13 +290,14 @@ __device__ __forceinline__ float one_minus_exp_neg(float x)
 
 // ---------------------------------------------------------------------------
 // Reset stream: counter-based. A reset of env `gid` in its episode `ep` seeds a
-// register-resident xoshiro128+ from splitmix64(seed, gid, ep, bits of the state being
-// replaced); no per-env RNG state lives in HBM and no memory access is needed.
+// register-resident xorshift128 (Marsaglia 2003) from four chained lowbias32 mixes of
+// (seed words, gid, ep, bits of the state being replaced); no per-env RNG state lives in
+// HBM and no memory access is needed. After the four mixes (8 quarter-rate
+// v_mul_lo_u32) every draw is 6 full-rate shift/xor ops; the top 24 bits of each draw
+// make one uniform (statistics: tests/test_gpu_envs.py::test_reset_distribution).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 
-// 32-bit avalanche mix (lowbias32). Each uniform of a reset is its own short chain,
-// so the 14 draws are independent instructions (ILP at one wave per SIMD).
+// 32-bit avalanche mix (lowbias32)
 __device__ __forceinline__ uint32_t mix32(uint32_t x)
 {
     x ^= x >> 16;
@@ -301,37 +308,31 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x)
     return x;
 }
 
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
-{
-    uint64_t z = x + 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-struct ResetKey {
-    uint32_t k0, k1;
-    // j-th uniform in [0, 1) with 24 random bits
-    __device__ __forceinline__ float uniform(uint32_t j) const
+struct ResetStream {
+    uint32_t x, y, z, w;
+    // next uniform in [0, 1) with 24 random bits
+    __device__ __forceinline__ float uniform()
     {
-        const uint32_t h = mix32(k0 + (j + 1u) * 0x9E3779B9u) ^ k1;
-        return (float)(h >> 8) * 0x1p-24f;
+        const uint32_t t = x ^ (x << 11);
+        x = y;
+        y = z;
+        z = w;
+        w = w ^ (w >> 19) ^ t ^ (t >> 8);
+        return (float)(w >> 8) * 0x1p-24f;
     }
 };
 
-__device__ __forceinline__ ResetKey reset_key(uint64_t seed, int64_t gid, uint32_t episode, float salt_a,
-                                              float salt_b)
+__device__ __forceinline__ ResetStream reset_stream(const uint32_t* seed_w, int64_t gid, uint32_t episode,
+                                                    float salt_a, float salt_b)
 {
-    uint64_t x = seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(gid + 1));
-    x ^= (uint64_t)episode * 0xA0761D6478BD642Full;
-    x ^= ((uint64_t)__float_as_uint(salt_a) << 32) | (uint64_t)__float_as_uint(salt_b);
-    const uint64_t a = splitmix64(x);
-    return ResetKey{(uint32_t)a, (uint32_t)(a >> 32)};
+    ResetStream r;
+    r.x = mix32((uint32_t)gid + seed_w[0]);
+    r.y = mix32(r.x ^ (episode + seed_w[1]) ^ (uint32_t)((uint64_t)gid >> 32));
+    r.z = mix32(r.y ^ __float_as_uint(salt_a) ^ seed_w[2]);
+    r.w = mix32(r.z ^ __float_as_uint(salt_b) ^ seed_w[3]);
+    return r;
 }
 
-// ---------------------------------------------------------------------------
-// Model traits
-// ---------------------------------------------------------------------------
 template <int MODEL>
 struct Dims;
 template <>
@@ -432,12 +433,107 @@ __device__ __forceinline__ void rhs(const KParams& P, const Ctl& c, const float*
     }
 }
 
+// 6DOF RK4 specialised to the structure of the RHS (simulator.py:259-294): r and v never
+// feed back (the aero force is identically zero, :359-360), so over one step they are
+// quadratures of the stage accelerations a_s = R(q_s) T_b / m_s + g:
+//   v1 = v0 + h/6 (a1 + 2 a2 + 2 a3 + a4),   r1 = r0 + h v0 + h^2/6 (a1 + a2 + a3)
+// (the RK4 update itself, rearranged); m is linear in t (exact at every stage); w1 is
+// constant (J2 == J3); q and (w2, w3) take the usual RK4 stages, carried as half-rates
+// W = w/2 so dq = Omega(W) q needs no 0.5 factors. Same RK4 solution as the generic form
+// below up to fp32 rounding. f0 = f(y0) for the event path.
+__device__ __forceinline__ void integrate6_rk4(const KParams& P, const Ctl& c, const float* y0, float* y1,
+                                               float* f0)
+{
+    const float h = P.h, hh = P.h2, h6 = P.h6, hh6 = P.h * P.h6;
+    const float t2x = 2.0f * c.tbx, t2y = 2.0f * c.tby, t2z = 2.0f * c.tbz;
+    // R(q) T_b / m + g with the unnormalised q (see rhs)
+    auto accel = [&](const float* q, float m, float* a) {
+        const float qq = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+        const float tx = q[2] * t2z - q[3] * t2y;
+        const float ty = q[3] * t2x - q[1] * t2z;
+        const float tz = q[1] * t2y - q[2] * t2x;
+        const float sc = frcp(qq * m);
+        a[0] = (qq * c.tbx + q[0] * tx + (q[2] * tz - q[3] * ty)) * sc - kG0;
+        a[1] = (qq * c.tby + q[0] * ty + (q[3] * tx - q[1] * tz)) * sc;
+        a[2] = (qq * c.tbz + q[0] * tz + (q[1] * ty - q[2] * tx)) * sc;
+    };
+    const float W1 = 0.5f * y0[10];
+    // dW2 = A2 + B2 W3, dW3 = A3 + B3 W2 (half of dw = J^-1 (tau - w x Jw))
+    const float A2 = 0.5f * c.tau1, B2 = (-2.0f * kJd1 * kJinv2) * W1;
+    const float A3 = 0.5f * c.tau2, B3 = (-2.0f * kJd2 * kJinv3) * W1;
+    auto dq = [&](const float* q, float W2, float W3, float* d) {
+        d[0] = -W1 * q[1] - W2 * q[2] - W3 * q[3];
+        d[1] = W1 * q[0] + W3 * q[2] - W2 * q[3];
+        d[2] = W2 * q[0] - W3 * q[1] + W1 * q[3];
+        d[3] = W3 * q[0] + W2 * q[1] - W1 * q[2];
+    };
+    const float* q0 = y0 + 6;
+    const float W20 = 0.5f * y0[11], W30 = 0.5f * y0[12], m0 = y0[13];
+    const float mh = m0 + hh * c.dm, me = m0 + h * c.dm;
+    float a1[3], a2[3], a3[3], a4[3], k1[4], k2[4], k3[4], k4[4], qs[4];
+    // stage 1
+    accel(q0, m0, a1);
+    dq(q0, W20, W30, k1);
+    const float l1 = A2 + B2 * W30, n1 = A3 + B3 * W20;
+    // stage 2
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qs[j] = q0[j] + hh * k1[j];
+    float W2s = W20 + hh * l1, W3s = W30 + hh * n1;
+    accel(qs, mh, a2);
+    dq(qs, W2s, W3s, k2);
+    const float l2 = A2 + B2 * W3s, n2 = A3 + B3 * W2s;
+    // stage 3
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qs[j] = q0[j] + hh * k2[j];
+    W2s = W20 + hh * l2;
+    W3s = W30 + hh * n2;
+    accel(qs, mh, a3);
+    dq(qs, W2s, W3s, k3);
+    const float l3 = A2 + B2 * W3s, n3 = A3 + B3 * W2s;
+    // stage 4
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qs[j] = q0[j] + h * k3[j];
+    W2s = W20 + h * l3;
+    W3s = W30 + h * n3;
+    accel(qs, me, a4);
+    dq(qs, W2s, W3s, k4);
+    const float l4 = A2 + B2 * W3s, n4 = A3 + B3 * W2s;
+    // updates
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float s23 = a2[j] + a3[j];
+        y1[3 + j] = y0[3 + j] + h6 * (a1[j] + a4[j] + 2.0f * s23);
+        y1[j] = (y0[j] + h * y0[3 + j]) + hh6 * (a1[j] + s23);
+        f0[j] = y0[3 + j];
+        f0[3 + j] = a1[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        y1[6 + j] = q0[j] + h6 * (k1[j] + k4[j] + 2.0f * (k2[j] + k3[j]));
+        f0[6 + j] = k1[j];
+    }
+    y1[10] = y0[10];
+    y1[11] = 2.0f * (W20 + h6 * (l1 + l4 + 2.0f * (l2 + l3)));
+    y1[12] = 2.0f * (W30 + h6 * (n1 + n4 + 2.0f * (n2 + n3)));
+    y1[13] = me;
+    f0[10] = 0.0f;
+    f0[11] = 2.0f * l1;
+    f0[12] = 2.0f * n1;
+    f0[13] = c.dm;
+}
+
 template <int MODEL, int INTEG>
 __device__ __forceinline__ void integrate(const KParams& P, const Ctl& c, const float* y0, float h,
                                           float* y1, float* f0)
 {
     constexpr int NS = Dims<MODEL>::NS;
     float k[NS], yt[NS];
+#if !RR_RK4_GENERIC
+    if constexpr (MODEL == 6 && INTEG == RR_INT_RK4) {
+        integrate6_rk4(P, c, y0, y1, f0);
+        return;
+    }
+#endif
     if constexpr (INTEG == RR_INT_EULER) {
         rhs<MODEL>(P, c, y0, k);
 #pragma unroll
@@ -500,7 +596,7 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         // inclusive. Fixed 3 iterations, branch-free (quadratic convergence from the secant
         // guess; the parity tests cover touchdowns down to |v| ~ 1 m/s).
 #pragma unroll
-        for (int it = 0; it < 3; ++it) {
+        for (int it = 0; it < RR_NEWTON_ITERS; ++it) {
             const float s2 = s * s, s3 = s2 * s;
             const float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
                             (s3 - s2) * hv1;
@@ -523,11 +619,11 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
 // Sample one initial condition: gym Box.sample (uniform in [low, high], float32),
 // then q <- q/|q| (rocket_env.py:672-673); v0 = |IC velocity| (rocket_env.py:989-991).
 template <int MODEL>
-__device__ __forceinline__ void sample_ic(const KParams& P, const ResetKey& k, float* s, float& v0)
+__device__ __forceinline__ void sample_ic(const KParams& P, ResetStream& k, float* s, float& v0)
 {
     constexpr int NS = Dims<MODEL>::NS;
 #pragma unroll
-    for (int j = 0; j < NS; ++j) s[j] = fmaf(P.ic_span[j], k.uniform(j), P.ic_low[j]);
+    for (int j = 0; j < NS; ++j) s[j] = fmaf(P.ic_span[j], k.uniform(), P.ic_low[j]);
     if constexpr (MODEL == 6) {
         const float rn = frsq(s[6] * s[6] + s[7] * s[7] + s[8] * s[8] + s[9] * s[9]);
         s[6] *= rn;
@@ -679,6 +775,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][EPW * NS];
+#if RR_DIAG == 7
+    return;  // launch + dispatch floor
+#endif
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = threadIdx.x / kWave;
     const uint32_t n = n_envs;
@@ -826,7 +925,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
         }
         if ((mode & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
-            const ResetKey key = reset_key(P.seed, P.id_off + i, ep, y1[0], y1[NS - 1]);
+            ResetStream key = reset_stream(P.seed_w, P.id_off + i, ep, y1[0], y1[NS - 1]);
             sample_ic<MODEL>(P, key, y1, v0);
             bst_f(st_r, v0, vo, v0_off);
             cw = ep << kEpisodeShift;
@@ -880,7 +979,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
     float s[NS], v0;
     if (mask == nullptr || mask[i]) {
         const uint32_t ep = (B.counter[i] >> kEpisodeShift) + 1u;
-        const ResetKey key = reset_key(P.seed, P.id_off + i, ep, B.state[i], B.state[(int64_t)(NS - 1) * n + i]);
+        ResetStream key = reset_stream(P.seed_w, P.id_off + i, ep, B.state[i], B.state[(int64_t)(NS - 1) * n + i]);
         sample_ic<MODEL>(P, key, s, v0);
 #pragma unroll
         for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = s[j];
@@ -950,6 +1049,22 @@ float floor_f(double d)  // largest float <= d
     return f;
 }
 
+// 64-bit user seed -> the reset stream's four key words (splitmix64, host side)
+void seed_words(uint64_t seed, uint32_t* w)
+{
+    auto sm = [](uint64_t x) {
+        uint64_t z = x + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    const uint64_t a = sm(seed), b = sm(seed + 0x9E3779B97F4A7C15ull);
+    w[0] = (uint32_t)a;
+    w[1] = (uint32_t)(a >> 32);
+    w[2] = (uint32_t)b;
+    w[3] = (uint32_t)(b >> 32);
+}
+
 KParams make_kparams(const rr_params& p)
 {
     KParams k;
@@ -1004,7 +1119,7 @@ KParams make_kparams(const rr_params& p)
     }
     k.omega_lt = ceil_f(p.omega_lim[0]);
     k.zero_h = floor_f(1e-3);
-    k.seed = 42;
+    seed_words(42, k.seed_w);
     k.id_off = 0;
     return k;
 }
@@ -1211,7 +1326,7 @@ int rr_seed(rr_env* e, uint64_t seed, void* stream)
 {
     (void)stream;  // the reset stream is counter-based: the seed is a kernel argument
     if (!e) return fail(RR_EINVAL, "rr_seed: null handle");
-    e->kp.seed = seed;
+    seed_words(seed, e->kp.seed_w);
     return RR_OK;
 }
 

@@ -180,3 +180,36 @@ def test_device_rollout_and_ppo_update():
     torch.cuda.synchronize()
     assert torch.isfinite(ro.rewards).all()
     env.close()
+
+
+@pytest.mark.parametrize("model", [6, 3])
+def test_reset_distribution(model):
+    """The counter-based reset stream draws init_space uniformly: per-component moments
+    of U(low, high), no cross-component correlation, q normalised (6DOF), and a new
+    draw per episode."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF, make_config
+
+    n = 1 << 20
+    kw = ENV_CONFIG_6DOF if model == 6 else {}
+    cfg = make_config(model, **kw)
+    b = RocketBatch(n, model=model, device="cuda:0", **kw)
+    b.reset()
+    s1 = b.get_state()[0].cpu().numpy().astype(np.float64)
+    b.reset()
+    s2 = b.get_state()[0].cpu().numpy().astype(np.float64)
+    b.close()
+    lo, hi = np.asarray(cfg.ic_low, np.float64), np.asarray(cfg.ic_high, np.float64)
+    comps = [j for j in range(cfg.state_dim) if hi[j] > lo[j] and not (model == 6 and 6 <= j < 10)]
+    for j in comps:
+        u = (s1[j] - lo[j]) / (hi[j] - lo[j])
+        assert u.min() >= 0 and u.max() <= 1
+        assert abs(u.mean() - 0.5) < 5 / np.sqrt(12 * n), (j, u.mean())
+        assert abs(u.var() * 12 - 1) < 0.01, (j, u.var())
+    c = np.corrcoef(s1[comps])
+    assert np.abs(c - np.eye(len(comps))).max() < 0.01
+    for j in comps:  # episode counter keys a fresh draw
+        assert abs(np.corrcoef(s1[j], s2[j])[0, 1]) < 0.01
+    if model == 6:
+        assert np.abs(np.linalg.norm(s1[6:10], axis=0) - 1).max() < 1e-5

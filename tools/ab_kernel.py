@@ -50,8 +50,8 @@ def main():
                 sys.exit(out.returncode)
             line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
             res[src].append(json.loads(line)["us_per_step"])
-    summary = {os.path.basename(s): {"median_us": statistics.median(v), "min_us": min(v), "runs": v}
-               for s, v in res.items()}
+    summary = {os.path.relpath(s.partition("@")[0], ROOT) + s.partition("@")[1] + s.partition("@")[2]:
+               {"median_us": statistics.median(v), "min_us": min(v), "runs": v} for s, v in res.items()}
     print(json.dumps({"n": a.n, "model": a.model, "variants": summary}, indent=1))
 
 
