@@ -45,6 +45,9 @@ namespace {
 #ifndef RR_RK4_GENERIC  // 1 = generic 14-component RK4 for 6DOF too (A/B reference)
 #define RR_RK4_GENERIC 0
 #endif
+#ifndef RR_EARLY_RESET  // 1 = draw the auto-reset candidate during the load wait
+#define RR_EARLY_RESET 1
+#endif
 #ifndef RR_NEWTON_ITERS
 #define RR_NEWTON_ITERS 3
 #endif
@@ -189,7 +192,7 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
 
 struct Bufs {
 #if RR_DIAG == 4
-    uint64_t* stamps;         // [waves][8]
+    uint64_t* stamps;         // [waves][10]: 8 s_memtime phase stamps, s_memrealtime at start / end
 #endif
     float* state;
     float* v0;
@@ -289,12 +292,14 @@ __device__ __forceinline__ float one_minus_exp_neg(float x)
 }
 
 // ---------------------------------------------------------------------------
-// Reset stream: counter-based. A reset of env `gid` in its episode `ep` seeds a
-// register-resident xorshift128 (Marsaglia 2003) from four chained lowbias32 mixes of
-// (seed words, gid, ep, bits of the state being replaced); no per-env RNG state lives in
-// HBM and no memory access is needed. After the four mixes (8 quarter-rate
-// v_mul_lo_u32) every draw is 6 full-rate shift/xor ops; the top 24 bits of each draw
-// make one uniform (statistics: tests/test_gpu_envs.py::test_reset_distribution).
+// Reset stream: counter-based. The initial condition an env `gid` gets when its episode
+// ends at counter word `cw` (episode | steps, unique per env and step) comes from a
+// register-resident xorshift128 (Marsaglia 2003) whose four words are chained lowbias32
+// mixes of (seed words, gid, cw): no per-env RNG state lives in HBM, the draw needs only
+// the counter word (so the step kernel draws it while the state planes are in flight),
+// and it is independent of how envs are sharded. After the mixes every draw is 6 full-rate
+// shift/xor ops; the top 24 bits of each draw make one uniform (statistics:
+// tests/test_gpu_envs.py::test_reset_distribution).
 // ---------------------------------------------------------------------------
 
 // 32-bit avalanche mix (lowbias32)
@@ -322,14 +327,16 @@ struct ResetStream {
     }
 };
 
-__device__ __forceinline__ ResetStream reset_stream(const uint32_t* seed_w, int64_t gid, uint32_t episode,
-                                                    float salt_a, float salt_b)
+__device__ __forceinline__ ResetStream reset_stream(const uint32_t* seed_w, int64_t gid, uint32_t cw)
 {
+    // every state word is a nonlinear function of (gid, cw): a word that depended on gid
+    // alone would correlate the components of one env's successive initial conditions
+    const uint32_t g = mix32(((uint32_t)gid + seed_w[0]) ^ (uint32_t)((uint64_t)gid >> 32));
     ResetStream r;
-    r.x = mix32((uint32_t)gid + seed_w[0]);
-    r.y = mix32(r.x ^ (episode + seed_w[1]) ^ (uint32_t)((uint64_t)gid >> 32));
-    r.z = mix32(r.y ^ __float_as_uint(salt_a) ^ seed_w[2]);
-    r.w = mix32(r.z ^ __float_as_uint(salt_b) ^ seed_w[3]);
+    r.x = mix32(g ^ (cw + seed_w[1]));
+    r.y = mix32(r.x ^ seed_w[2]);
+    r.z = mix32(r.y ^ seed_w[3]);
+    r.w = mix32(r.z ^ seed_w[0]);
     return r;
 }
 
@@ -676,7 +683,9 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         float R22 = w * w - x * x - y * y + z * z;
         float ra = fsqrt(R00 * R00 + mR01 * mR01);
         float rc = fsqrt(R22 * R22 + mR12 * mR12);
-        float sb = fabsf(R02) / qq;
+        // q was renormalised after the step (|q|^2 = 1 to fp32 rounding), so sin b = R02
+        // without the division by |q|^2 (R00, R22 and the cos b radii are homogeneous)
+        float sb = fabsf(R02);
         bool att = (!(P.att_never & 1u) && R00 < ra * P.att_c[0]) || (!(P.att_never & 2u) && sb > P.att_c[1]) ||
                    (!(P.att_never & 4u) && R22 < rc * P.att_c[2]);
         t[3] = att ? P.gamma : 0.0f;
@@ -768,7 +777,10 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
 // preloads them into user SGPRs at wave launch (-mllvm -amdgpu-kernarg-preload-count,
 // rl_rocket_amd/build.py): the first state loads then issue without waiting for scalar
 // loads of the kernarg segment. `mode` = rr_params.flags | kModeCounter.
-template <int MODEL, int INTEG, int EPW = kWave>
+// ASOA: action layout [NA][N] (RR_FLAG_ACTION_SOA) as a template parameter: a runtime
+// branch between the two layouts made the waitcnt pass stall the wave on the state loads
+// before it issued the action load (two serial memory round trips).
+template <int MODEL, int INTEG, bool ASOA, int EPW = kWave>
 __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state, const float* __restrict__ action,
                                                       uint32_t n_envs, uint32_t mode, const KParams P, const Bufs B,
                                                       const StepIO io)
@@ -796,12 +808,28 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
     const rsrc_t act_r = make_rsrc(action, (uint64_t)NA * plane);
     const uint32_t v0_off = NS * plane, cw_off = (NS + 1) * plane, ret_off = (NS + 2) * plane;
 #if RR_DIAG == 4
-    uint64_t stamp_[8];
+    uint64_t stamp_[8], rt0_;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0_)::"memory");
 #endif
     RR_STAMP(0);
 
-    // ---- all loads first (one memory round trip per wave) ----
+    // ---- all loads first (one memory round trip per wave); the counter word first, so the
+    // reset candidate below is drawn while the state planes are still in flight ----
+    uint32_t cw = use_counter ? bld_u(st_r, vo, cw_off) : 0u;
     float y0[NS], y1[NS], f0[NS], a[NA];
+    if constexpr (ASOA) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
+    } else if constexpr (NA == 3) {
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)((vo << 1) + vo), 0, RR_LD_AUX);  // 12 B rows
+        a[0] = __uint_as_float(v.x);
+        a[1] = __uint_as_float(v.y);
+        a[2] = __uint_as_float(v.z);
+    } else {
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(vo << 1), 0, RR_LD_AUX);  // 8 B rows
+        a[0] = __uint_as_float(v.x);
+        a[1] = __uint_as_float(v.y);
+    }
 #if RR_DIAG == 3
 #pragma unroll
     for (int j = 0; j < NS; ++j) y0[j] = P.ic_low[j] + P.ic_span[j] * (float)(lane & 15) * (1.0f / 16.0f);
@@ -809,23 +837,19 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
 #pragma unroll
     for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
 #endif
-    if (mode & RR_FLAG_ACTION_SOA) {
-#pragma unroll
-        for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
-    } else if constexpr (NA == 3) {
-        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)(ic * 12u), 0, RR_LD_AUX);
-        a[0] = __uint_as_float(v.x);
-        a[1] = __uint_as_float(v.y);
-        a[2] = __uint_as_float(v.z);
-    } else {
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(ic * 8u), 0, RR_LD_AUX);
-        a[0] = __uint_as_float(v.x);
-        a[1] = __uint_as_float(v.y);
-    }
     float v0 = bld_f(st_r, vo, v0_off);
-    uint32_t cw = use_counter ? bld_u(st_r, vo, cw_off) : 0u;
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
+#if RR_EARLY_RESET
+    // SB3 auto-reset candidate of this step, keyed on (gid, counter word): ~200 VALU that
+    // fill the wait for the state planes instead of lengthening the done branch of the
+    // waves that finish last (RR_DIAG=4 stamps: 1560 cycles). Used by done lanes only.
+    float ic_s[NS], ic_v0 = 0.0f;
+    if (mode & RR_FLAG_AUTO_RESET) {
+        ResetStream key = reset_stream(P.seed_w, P.id_off + i, cw);
+        sample_ic<MODEL>(P, key, ic_s, ic_v0);
+    }
+#endif
 #if RR_DIAG == 4
     {  // force every load to land, then stamp
         float sum_ = v0 + (float)cw + ret;
@@ -911,22 +935,36 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
     }
     if (m) {
         if (dv) {
-            float2* to = reinterpret_cast<float2*>(B.term_obs + (size_t)i * NS);  // NS even or not: 8-B aligned rows
-            if constexpr (NS % 2 == 0) {
+            // row i of [N][NS]: 16-B stores (rows are 4-B aligned; gfx950 buffer stores
+            // need only dword alignment), NS = 14 -> 3 x 16 B + 8 B, NS = 7 -> 16 B + 12 B
+            const rsrc_t tr = make_rsrc(B.term_obs, (uint64_t)NS * plane);
+            const uint32_t ro = i * (NS * 4u);
+            auto u4 = [&](int j) {
+                return u32x4{__float_as_uint(o[j]), __float_as_uint(o[j + 1]), __float_as_uint(o[j + 2]),
+                             __float_as_uint(o[j + 3])};
+            };
 #pragma unroll
-                for (int j = 0; j < NS / 2; ++j) to[j] = make_float2(o[2 * j], o[2 * j + 1]);
-            } else {
-                float* tf = B.term_obs + (size_t)i * NS;
-#pragma unroll
-                for (int j = 0; j < NS; ++j) tf[j] = o[j];
-            }
+            for (int j = 0; j + 4 <= NS; j += 4) __builtin_amdgcn_raw_buffer_store_b128(u4(j), tr, (int)(ro + j * 4), 0, 0);
+            if constexpr (NS % 4 == 2)
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
+                                                      (int)(ro + (NS - 2) * 4), 0, 0);
+            else if constexpr (NS % 4 == 3)
+                __builtin_amdgcn_raw_buffer_store_b96(
+                    u32x3{__float_as_uint(o[NS - 3]), __float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
+                    (int)(ro + (NS - 3) * 4), 0, 0);
             B.term_ret[i] = ret;
             B.term_len[i] = el;
         }
         if ((mode & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
-            ResetStream key = reset_stream(P.seed_w, P.id_off + i, ep, y1[0], y1[NS - 1]);
+#if RR_EARLY_RESET
+#pragma unroll
+            for (int j = 0; j < NS; ++j) y1[j] = ic_s[j];
+            v0 = ic_v0;
+#else
+            ResetStream key = reset_stream(P.seed_w, P.id_off + i, cw);
             sample_ic<MODEL>(P, key, y1, v0);
+#endif
             bst_f(st_r, v0, vo, v0_off);
             cw = ep << kEpisodeShift;
 #pragma unroll
@@ -961,9 +999,13 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
 #if RR_DIAG == 4
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     RR_STAMP(7);
+    uint64_t rt1_;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1_)::"memory");
     if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 8 + k] = stamp_[k];
+        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 10 + k] = stamp_[k];
+        B.stamps[(size_t)wave_idx * 10 + 8] = rt0_;
+        B.stamps[(size_t)wave_idx * 10 + 9] = rt1_;
     }
 #endif
 }
@@ -979,7 +1021,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
     float s[NS], v0;
     if (mask == nullptr || mask[i]) {
         const uint32_t ep = (B.counter[i] >> kEpisodeShift) + 1u;
-        ResetStream key = reset_stream(P.seed_w, P.id_off + i, ep, B.state[i], B.state[(int64_t)(NS - 1) * n + i]);
+        ResetStream key = reset_stream(P.seed_w, P.id_off + i, B.counter[i]);
         sample_ic<MODEL>(P, key, s, v0);
 #pragma unroll
         for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = s[j];
@@ -1264,7 +1306,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
 #if RR_DIAG == 4
-        {(void**)&e->stamps, sizeof(uint64_t) * 8 * n_words(n)},
+        {(void**)&e->stamps, sizeof(uint64_t) * 10 * n_words(n)},
 #endif
     };
     const bool exact = p->integrator == RR_INT_DOPRI5;
@@ -1369,16 +1411,23 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
         const uint32_t nn = (uint32_t)e->n;
         const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
         const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
-        if (m6 && !euler)
-            hipLaunchKernelGGL((step_kernel<6, RR_INT_RK4>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b, io);
-        else if (m6)
-            hipLaunchKernelGGL((step_kernel<6, RR_INT_EULER>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b,
-                               io);
-        else if (!euler)
-            hipLaunchKernelGGL((step_kernel<3, RR_INT_RK4>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b, io);
-        else
-            hipLaunchKernelGGL((step_kernel<3, RR_INT_EULER>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b,
-                               io);
+        const bool soa = e->p.flags & RR_FLAG_ACTION_SOA;
+#define RR_LAUNCH(M, I, A) \
+    hipLaunchKernelGGL((step_kernel<M, I, A>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b, io)
+        if (m6 && !euler) {
+            if (soa) RR_LAUNCH(6, RR_INT_RK4, true);
+            else RR_LAUNCH(6, RR_INT_RK4, false);
+        } else if (m6) {
+            if (soa) RR_LAUNCH(6, RR_INT_EULER, true);
+            else RR_LAUNCH(6, RR_INT_EULER, false);
+        } else if (!euler) {
+            if (soa) RR_LAUNCH(3, RR_INT_RK4, true);
+            else RR_LAUNCH(3, RR_INT_RK4, false);
+        } else {
+            if (soa) RR_LAUNCH(3, RR_INT_EULER, true);
+            else RR_LAUNCH(3, RR_INT_EULER, false);
+        }
+#undef RR_LAUNCH
     }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return hip_fail(err, "rr_step: launch");
@@ -1553,9 +1602,9 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
 // diagnostic build only: copy the per-wave phase stamps of the last step to the host
 int64_t rr_debug_stamps(rr_env* e, uint64_t* host, int64_t cap)
 {
-    const int64_t nw = std::min<int64_t>(cap / 8, n_words(e->n));
+    const int64_t nw = std::min<int64_t>(cap / 10, n_words(e->n));
     hipError_t err = hipDeviceSynchronize();
-    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 8 * nw, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 10 * nw, hipMemcpyDeviceToHost);
     return err == hipSuccess ? nw : hip_fail(err, "rr_debug_stamps");
 }
 #endif

@@ -70,6 +70,19 @@ def main():
     out["wave_life_us_median"] = float(np.median([np.median(e - s) for s, e in zip(rt, rte)]))
     out["wave_life_cycles_median"] = float(np.median(per[:, :, 7] - per[:, :, 0]))
     out["clock_ghz"] = out["wave_life_cycles_median"] / out["wave_life_us_median"] / 1e3
+    # the wave that finishes last sets the kernel time: its start and phase breakdown
+    crit = []
+    for p in per:
+        w = int(np.argmax(p[:, 9]))
+        ph = np.diff(p[w, :8])
+        crit.append([(p[w, 8] - p[:, 8].min()) / 100.0, (p[w, 9] - p[w, 8]) / 100.0] + list(ph))
+    crit = np.median(np.array(crit, np.float64), axis=0)
+    out["critical_wave"] = {"start_us": crit[0], "life_us": crit[1],
+                            "phases_cycles": dict(zip(names, [float(x) for x in crit[2:]]))}
+    ev = d[:, 2] > 400  # waves that ran the event path
+    rs = d[:, 4] > 400  # waves that ran the reset path
+    out["frac_waves_event"] = float(ev.mean())
+    out["frac_waves_reset"] = float(rs.mean())
     print(json.dumps(out, indent=1))
     env.close()
 
