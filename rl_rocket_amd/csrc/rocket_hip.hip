@@ -32,7 +32,8 @@
 //   1 = memory only (no integration / reward arithmetic), 2 = no event / reset branches,
 //   3 = compute only (state synthesised in registers instead of loaded),
 //   4 = product kernel + s_memtime phase stamps per wave (rr_debug_stamps),
-//   5 = no event path, 6 = no in-kernel reset, 7 = empty kernel (launch + dispatch floor).
+//   5 = no event path, 6 = no in-kernel reset, 7 = empty kernel (launch + dispatch floor),
+//   8 = empty kernel allocating RR_DIAG8_V + 1 VGPRs.
 #ifndef RR_DIAG
 #define RR_DIAG 0
 #endif
@@ -648,22 +649,20 @@ template <int MODEL>
 __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s, const float* a, float v0,
                                               bool& bounds_violation, float* t)
 {
+    // Branch-free on purpose: the comparisons combine with bitwise & / | and the waypoint
+    // cases with selects, so a lone wave runs straight-line code (short-circuit && / ||
+    // compiled to ~8 exec-mask branches here).
     if constexpr (MODEL == 6) {
         // _check_bounds_violation: Box(lo, hi, float32).contains(r) (rocket_env.py:1036-1038)
-        bool inside = s[0] >= P.blo[0] && s[0] <= P.bhi[0] && s[1] >= P.blo[1] && s[1] <= P.bhi[1] &&
-                      s[2] >= P.blo[2] && s[2] <= P.bhi[2];
+        const bool inside = (s[0] >= P.blo[0]) & (s[0] <= P.bhi[0]) & (s[1] >= P.blo[1]) & (s[1] <= P.bhi[1]) &
+                            (s[2] >= P.blo[2]) & (s[2] <= P.bhi[2]);
         bounds_violation = !inside;
         // _compute_vtarg (rocket_env.py:986-1014)
-        float rh0, rh1, rh2, vh0, tau_inv;
-        if (s[0] > P.waypoint) {
-            rh0 = s[0] - P.waypoint; rh1 = s[1]; rh2 = s[2];
-            vh0 = s[3] + 2.0f;
-            tau_inv = 1.0f / 20.0f;
-        } else {
-            rh0 = s[0] + 1.0f; rh1 = 0.0f; rh2 = 0.0f;
-            vh0 = s[3] + 1.0f;
-            tau_inv = 1.0f / 100.0f;
-        }
+        const bool above = s[0] > P.waypoint;
+        const float rh0 = above ? s[0] - P.waypoint : s[0] + 1.0f;
+        const float rh1 = above ? s[1] : 0.0f, rh2 = above ? s[2] : 0.0f;
+        const float vh0 = s[3] + (above ? 2.0f : 1.0f);
+        const float tau_inv = above ? 1.0f / 20.0f : 1.0f / 100.0f;
         float nrh = fsqrt(rh0 * rh0 + rh1 * rh1 + rh2 * rh2);
         float t_go = nrh * frsq(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
         float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * one_minus_exp_neg(t_go * tau_inv);
@@ -675,7 +674,6 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         // zyx Euler angles of q (Rotation.as_euler("zyx"), rocket_env.py:852-855, 1047):
         //   a = atan2(-R01, R00), b = asin(R02), c = atan2(-R12, R22)
         const float w = s[6], x = s[7], y = s[8], z = s[9];
-        float qq = w * w + x * x + y * y + z * z;
         float R00 = w * w + x * x - y * y - z * z;
         float mR01 = 2.0f * (z * w - x * y);
         float R02 = 2.0f * (x * z + y * w);
@@ -686,33 +684,28 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         // q was renormalised after the step (|q|^2 = 1 to fp32 rounding), so sin b = R02
         // without the division by |q|^2 (R00, R22 and the cos b radii are homogeneous)
         float sb = fabsf(R02);
-        bool att = (!(P.att_never & 1u) && R00 < ra * P.att_c[0]) || (!(P.att_never & 2u) && sb > P.att_c[1]) ||
-                   (!(P.att_never & 4u) && R22 < rc * P.att_c[2]);
+        const bool att = (!(P.att_never & 1u) & (R00 < ra * P.att_c[0])) | (!(P.att_never & 2u) & (sb > P.att_c[1])) |
+                         (!(P.att_never & 4u) & (R22 < rc * P.att_c[2]));
         t[3] = att ? P.gamma : 0.0f;
         // _check_landing (rocket_env.py:1040-1061); any() over angles and omega is the reference's
-        bool att_ok = (P.land_always & 1u) || R00 > ra * P.land_c[0] || (P.land_always & 2u) ||
-                      sb < P.land_c[1] || (P.land_always & 4u) || R22 > rc * P.land_c[2];
-        bool om_ok = fabsf(s[10]) < P.omega_lt || fabsf(s[11]) < P.omega_lt || fabsf(s[12]) < P.omega_lt;
+        const bool att_ok = (P.land_always != 0u) | (R00 > ra * P.land_c[0]) | (sb < P.land_c[1]) |
+                            (R22 > rc * P.land_c[2]);
+        const bool om_ok = (fabsf(s[10]) < P.omega_lt) | (fabsf(s[11]) < P.omega_lt) | (fabsf(s[12]) < P.omega_lt);
         float r2 = s[0] * s[0] + s[1] * s[1] + s[2] * s[2];
         float v2 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
-        bool landing = s[0] <= P.zero_h && v2 < P.land_v2 && r2 < P.land_r2 && att_ok && om_ok;
+        const bool landing = (s[0] <= P.zero_h) & (v2 < P.land_v2) & (r2 < P.land_r2) & att_ok & om_ok;
         t[4] = landing ? P.kappa : 0.0f;
         if (P.flags & RR_FLAG_REWARD_ANNEALING) return t[3] + t[4] - P.xi * (a[2] + 1.0f);
         return t[0] + t[1] + t[2] + t[3] + t[4] + (bounds_violation ? -50.0f : 0.0f);
     } else {
         // _check_bounds (rocket_env.py:431-447)
-        bounds_violation = s[0] <= P.blo[0] || s[0] >= P.bhi[0] || s[1] >= P.bhi[1];
+        bounds_violation = (s[0] <= P.blo[0]) | (s[0] >= P.bhi[0]) | (s[1] >= P.bhi[1]);
         // _compute_vtarg (rocket_env.py:219-247)
-        float rh0, rh1, vh1, tau_inv;
-        if (s[1] > P.waypoint) {
-            rh0 = s[0]; rh1 = s[1] - P.waypoint;
-            vh1 = s[4] + 2.0f;
-            tau_inv = 1.0f / 20.0f;
-        } else {
-            rh0 = 0.0f; rh1 = s[1];
-            vh1 = s[4] + 1.0f;
-            tau_inv = 1.0f / 100.0f;
-        }
+        const bool above = s[1] > P.waypoint;
+        const float rh0 = above ? s[0] : 0.0f;
+        const float rh1 = above ? s[1] - P.waypoint : s[1];
+        const float vh1 = s[4] + (above ? 2.0f : 1.0f);
+        const float tau_inv = above ? 1.0f / 20.0f : 1.0f / 100.0f;
         float nrh = fsqrt(rh0 * rh0 + rh1 * rh1);
         float nvh = fsqrt(s[3] * s[3] + vh1 * vh1);
         float t_go = nrh * frcp(nvh);
@@ -727,8 +720,8 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         // _check_landing (rocket_env.py:449-476)
         float r2 = s[0] * s[0] + s[1] * s[1];
         float v2 = s[3] * s[3] + s[4] * s[4];
-        bool landing = s[1] <= P.zero_h && v2 < P.land_v2 && r2 < P.land_r2 && zeta < 0.2f &&
-                       fabsf(s[5]) < P.omega_lt;
+        const bool landing = (s[1] <= P.zero_h) & (v2 < P.land_v2) & (r2 < P.land_r2) & (zeta < 0.2f) &
+                             (fabsf(s[5]) < P.omega_lt);
         t[5] = landing ? P.kappa : 0.0f;
         if (P.flags & RR_FLAG_REWARD_ANNEALING) return t[3] + t[5] - P.xi * (a[1] + 1.0f);
         return t[0] + t[1] + t[2] + t[3] + t[4] + t[5] + (bounds_violation ? -50.0f : 0.0f);
@@ -790,8 +783,16 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
 #if RR_DIAG == 7
     return;  // launch + dispatch floor
 #endif
+#if RR_DIAG == 8  // empty kernel that allocates RR_DIAG8_V + 1 VGPRs: dispatch cost vs VGPR count
+#define RR_STR2(x) #x
+#define RR_STR(x) RR_STR2(x)
+    asm volatile("s_nop 0" ::: "v" RR_STR(RR_DIAG8_V));
+    return;
+#endif
     const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wv = threadIdx.x / kWave;
+    // wave index as an SGPR: derived from threadIdx it is a VGPR the compiler cannot prove
+    // uniform, and every buffer store with a wave_base soffset became a waterfall loop
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t n = n_envs;
     const uint32_t wave_idx = blockIdx.x * kWavesPerBlock + wv;
     const uint32_t wave_base = wave_idx * EPW;
@@ -848,6 +849,13 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
     if (mode & RR_FLAG_AUTO_RESET) {
         ResetStream key = reset_stream(P.seed_w, P.id_off + i, cw);
         sample_ic<MODEL>(P, key, ic_s, ic_v0);
+#if RR_EARLY_RESET == 2
+        // park the candidate in this wave's (still unused) obs-tile LDS, plane-major so the
+        // accesses are bank-conflict free; it is read back only by lanes that reset
+#pragma unroll
+        for (int j = 0; j < NS; ++j)
+            if (lane < (uint32_t)EPW) lds[wv][j * EPW + lane] = ic_s[j];
+#endif
     }
 #endif
 #if RR_DIAG == 4
@@ -957,7 +965,11 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
         }
         if ((mode & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
-#if RR_EARLY_RESET
+#if RR_EARLY_RESET == 2
+#pragma unroll
+            for (int j = 0; j < NS; ++j) y1[j] = lds[wv][j * EPW + lane];
+            v0 = MODEL == 6 ? fsqrt(y1[3] * y1[3] + y1[4] * y1[4] + y1[5] * y1[5]) : fsqrt(y1[3] * y1[3] + y1[4] * y1[4]);
+#elif RR_EARLY_RESET
 #pragma unroll
             for (int j = 0; j < NS; ++j) y1[j] = ic_s[j];
             v0 = ic_v0;
