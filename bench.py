@@ -106,10 +106,19 @@ def bench_rollout(args, dev, n, model, kw):
     }
 
 
-def cpu_baseline(model, seconds, seed=0):
-    """The CPU oracle (faithful scipy-RK45 restatement in C, 1 thread) stepping a
-    bounded sample of the same workload: envs from the same init_space, U(-1,1)
-    actions, auto-reset on done, TimeLimit 800."""
+def host_cores():
+    """CPU threads this process may use (the GPU box shows the whole machine in
+    os.cpu_count(); its share is the affinity mask / OMP_NUM_THREADS)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else max(1, min(n, 16))
+
+
+def cpu_baseline(model, seconds, seed=0, nthreads=1, n=1024):
+    """The CPU oracle (faithful scipy-RK45 restatement in C) stepping a bounded sample of
+    the same workload: envs from the same init_space, U(-1,1) actions, auto-reset on done,
+    TimeLimit 800; `nthreads` OpenMP threads over the env batch (SURVEY.md §8d baselines
+    (i) 1 core and (ii) all host cores)."""
     import numpy as np
 
     from oracle import oracle as O
@@ -123,7 +132,6 @@ def cpu_baseline(model, seconds, seed=0):
     lo_ic = (np.float32(kw["IC"]) - np.float32(kw["ICRange"]) / 2).astype(np.float32)
     hi_ic = (np.float32(kw["IC"]) + np.float32(kw["ICRange"]) / 2).astype(np.float32)
     rng = np.random.default_rng(seed)
-    n = 1024
 
     def sample(k):
         ic = rng.uniform(lo_ic, hi_ic, (k, ns)).astype(np.float32)
@@ -140,7 +148,7 @@ def cpu_baseline(model, seconds, seed=0):
     while busy < seconds:
         a = rng.uniform(-1, 1, (n, na)).astype(np.float32)
         t0 = time.perf_counter()
-        out = O.step(cfg, ic, t, s, a, nthreads=1)
+        out = O.step(cfg, ic, t, s, a, nthreads=nthreads)
         busy += time.perf_counter() - t0
         steps += n
         s = out["state_out"]
@@ -153,11 +161,11 @@ def cpu_baseline(model, seconds, seed=0):
             s[d] = ic[d]
             el[d] = 0
             t[d] = 0
-    return {"value": steps / busy, "unit": "env-steps/s", "cores": 1, "kind": "port",
+    return {"value": steps / busy, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
             "sample": "%d env-steps of %s (%d envs x %d steps, env_config ICs, U(-1,1) actions, auto-reset, "
-                      "TimeLimit 800) through oracle/librocket_oracle.so ro_step_batch, 1 thread; "
+                      "TimeLimit 800) through oracle/librocket_oracle.so ro_step_batch, %d thread(s); "
                       "reference Python step() measured 569 (6DOF) / 3396 (3DOF) steps/s/core in the survey "
-                      "container (BASELINE.md)" % (steps, "6DOF" if model == 6 else "3DOF", n, steps // n)}
+                      "container (BASELINE.md)" % (steps, "6DOF" if model == 6 else "3DOF", n, steps // n, nthreads)}
 
 
 def stored_traffic(model, n):
@@ -299,6 +307,11 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.cpu_seconds)
+        c = host_cores()
+        if c > 1:  # SURVEY.md §8d baseline (ii): the batched oracle on all host cores
+            result["cpu_baseline"]["all_cores"] = {
+                k: v for k, v in cpu_baseline(model, max(2.0, args.cpu_seconds / 3), nthreads=c, n=8192).items()
+                if k in ("value", "unit", "cores", "sample")}
     env.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
