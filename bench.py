@@ -189,12 +189,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for the N > 1 path on a one-GPU box (not used by the driver's runs):
+    # RR_BENCH_ONE_DEVICE=1 puts every rank on cuda:0, RR_BENCH_BACKEND=gloo replaces RCCL
+    # (RCCL refuses two ranks on one GPU). Default: one GPU per rank over RCCL.
+    if os.environ.get("RR_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("RR_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF, MAX_EPISODE_STEPS, parse_model
@@ -268,8 +277,8 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if dist is not None:  # max over ranks of the timed region
+        t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 

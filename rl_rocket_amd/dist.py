@@ -38,6 +38,10 @@ class ShardGather:
     def _gather(self, out, t):
         if self._into:
             self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        elif out.is_cuda:  # gloo moves host tensors only: stage through the host (CPU rehearsal path)
+            host = out.cpu()
+            self.dist.all_gather(list(host.chunk(self.world)), t.cpu().contiguous(), group=self.group)
+            out.copy_(host)
         else:
             self.dist.all_gather(list(out.chunk(self.world)), t.contiguous(), group=self.group)
 
