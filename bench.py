@@ -45,6 +45,8 @@ def parse():
                     help="step: the fused env step (headline); rollout: on-device PPO rollout "
                          "collection (MlpPolicy 64x64 forward + sample + env step + buffer), BASELINE configs[4]")
     ap.add_argument("--rollout-steps", type=int, default=16)
+    ap.add_argument("--rollout-torch", action="store_true",
+                    help="rollout policy / bootstrap / GAE as PyTorch ops instead of the fused HIP kernels")
     return ap.parse_args()
 
 
@@ -62,7 +64,7 @@ def bench_rollout(args, dev, n, model, kw):
     env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
                       episode_stats=False, integrator=args.integrator, **kw)
     pol = MlpActorCritic(env.state_dim, env.action_dim).to(dev)
-    ro = DeviceRollout(env, pol, n_steps=args.rollout_steps)
+    ro = DeviceRollout(env, pol, n_steps=args.rollout_steps, fused=not args.rollout_torch)
     for _ in range(3):
         ro.collect()
     torch.cuda.synchronize(dev)
@@ -100,7 +102,8 @@ def bench_rollout(args, dev, n, model, kw):
         "dtype": "fp32", "data": "synthetic ICs (env_config init_space), actions from a random-init MlpPolicy",
         "config": {"workload": "Rocket6DOF N=%d, MlpPolicy(64x64 tanh) forward + Gaussian sample + fused step "
                                "+ timeout bootstrap + rollout buffer + GAE, n_steps=%d per hipGraph"
-                               % (n, args.rollout_steps), "envs_per_gpu": n},
+                               % (n, args.rollout_steps), "envs_per_gpu": n,
+                   "policy_path": "PyTorch ops" if args.rollout_torch else "fused HIP (fp32 MFMA) rr_policy_act"},
         "gpu_ms_per_collect": e0.elapsed_time(e1) / reps,
         "ppo_epoch_ms": upd * 1e3, "ppo_stats": stats,
     }

@@ -176,6 +176,40 @@ int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs
  * (rows valid where done[i]); any destination may be NULL. Asynchronous. */
 int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* term_len, void* stream);
 
+/* ---- On-device PPO rollouts (BASELINE configs[4]) ----
+ * Replace the per-step host work of stable_baselines3 1.6 OnPolicyAlgorithm.collect_rollouts
+ * + RolloutBuffer (the reference trains PPO("MlpPolicy", ...), main_6DOF.py:110-116) for
+ * an on-device rollout: the MlpPolicy actor-critic (separate pi / vf towers, net_arch
+ * [64, 64], tanh, state-independent log_std) runs as one fp32 MFMA launch per step.
+ * Supported (obs_dim, act_dim): (14, 3) 6DOF, (7, 2) 3DOF. */
+
+/* Packed parameter buffer for rr_policy_*: returns its size in floats (or RR_EINVAL) and,
+ * if off != NULL, the 12 section offsets {L1A, B1, L2A, B2, TOWER, PI, VF, HA, HV, HB, VB,
+ * LS} (fragment-ordered layout, rl_rocket_amd/csrc/rocket_policy.inc; filled on the device
+ * by rl_rocket_amd.rollout.pack_policy). Host-only. */
+int rr_policy_layout(int obs_dim, int act_dim, int64_t* off);
+
+/* Policy forward + Gaussian sample for n envs (SB3 ActorCriticPolicy.forward + clip):
+ *   obs [n][obs_dim] -> action_env [n][act_dim] (clip to [-1, 1], the rr_step input),
+ *   action [n][act_dim] (unclipped sample), value [n], log_prob [n], obs_copy [n][obs_dim]
+ *   (or NULL; the rollout buffer's obs[t]). The normal draws are counter-based on
+ *   (seed, env_id_offset + i, *iter, t): `iter` is a device uint64 the caller advances once
+ *   per rollout, so graph replays draw new noise. params 16-B aligned. */
+int rr_policy_act(const float* params, int obs_dim, int act_dim, int64_t n, int64_t env_id_offset, const float* obs,
+                  uint64_t seed, const uint64_t* iter, int t, float* action_env, float* action, float* value,
+                  float* log_prob, float* obs_copy, void* stream);
+
+/* Timeout bootstrap of collect_rollouts: reward_out[i] = reward[i] + gamma * V(term_obs[i])
+ * where truncated[i] (TimeLimit.truncated), else reward[i]. */
+int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int64_t n, const float* term_obs,
+                        const uint8_t* truncated, const float* reward, float gamma, float* reward_out, void* stream);
+
+/* RolloutBuffer.compute_returns_and_advantage: rewards / values / starts [T][n] (starts[t]
+ * = episode-start flag of step t), last_value / last_done [n] -> advantages, returns [T][n]. */
+int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, const float* starts,
+           const float* last_value, const float* last_done, float gamma, float lam, float* advantages,
+           float* returns, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

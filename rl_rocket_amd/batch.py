@@ -46,6 +46,7 @@ class RocketBatch:
         _lib.check(self.lib.rr_create(ctypes.byref(h), ctypes.byref(self.params), self.num_envs, int(env_id_offset),
                                       device.index), "rr_create")
         self._h = h
+        self.env_id_offset = int(env_id_offset)
         n, ns = self.num_envs, self.state_dim
         kw = dict(device=device)
         self.obs = torch.empty((n, ns), dtype=torch.float32, **kw)

@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "rocket_hip.hip")
-DEPS = [os.path.join(HERE, "csrc", "rocket_dopri5.inc")]
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc")]
 HEADER = os.path.join(ROOT, "include", "rocket_hip.h")
 OUT = os.path.join(HERE, "librocket_hip.so")
 ARCH = os.environ.get("RR_OFFLOAD_ARCH", "gfx950")

@@ -1068,6 +1068,9 @@ __global__ __launch_bounds__(kBlock) void gather_done_kernel(const int32_t* idx,
     g_len[k] = term_len[i];
 }
 
+// On-device PPO rollout kernels (fused MlpPolicy forward on fp32 MFMA, bootstrap, GAE)
+#include "rocket_policy.inc"
+
 // Exact-integrator mode (RR_INT_DOPRI5): fp64 scipy RK45 restatement, compiled without
 // FMA contraction so its roundings follow the reference's numpy arithmetic.
 #pragma clang fp contract(off)
@@ -1608,6 +1611,78 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
     if (err == hipSuccess && term_len)
         err = hipMemcpyAsync(term_len, e->term_len, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_copy_terminal");
+}
+
+// ---- on-device PPO rollout (rocket_policy.inc) ----
+
+int rr_policy_layout(int obs_dim, int act_dim, int64_t* off)
+{
+    auto fill = [&](auto L) {
+        using LL = decltype(L);
+        if (off) {
+            const int64_t v[12] = {LL::L1A, LL::B1, LL::L2A, LL::B2, LL::TOWER, LL::PI,
+                                   LL::VF,  LL::HA, LL::HV,  LL::HB, LL::VB,    LL::LS};
+            for (int k = 0; k < 12; ++k) off[k] = v[k];
+        }
+        return (int)LL::SIZE;
+    };
+    if (obs_dim == 14 && act_dim == 3) return fill(pol::Layout<14, 3>{});
+    if (obs_dim == 7 && act_dim == 2) return fill(pol::Layout<7, 2>{});
+    return fail(RR_EINVAL, "rr_policy_layout: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+}
+
+int rr_policy_act(const float* params, int obs_dim, int act_dim, int64_t n, int64_t env_id_offset, const float* obs,
+                  uint64_t seed, const uint64_t* iter, int t, float* action_env, float* action, float* value,
+                  float* log_prob, float* obs_copy, void* stream)
+{
+    if (!params || !obs || !iter || !action_env || !action || !value || !log_prob || n <= 0)
+        return fail(RR_EINVAL, "rr_policy_act: null argument or n <= 0");
+    if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_policy_act: params must be 16-B aligned");
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock)), block(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
+    if (obs_dim == 14 && act_dim == 3)
+        hipLaunchKernelGGL((policy_act_kernel<14, 3>), grid, block, 0, s, params, n, env_id_offset, obs, lo, hi, iter,
+                           (uint32_t)t, action_env, action, value, log_prob, obs_copy);
+    else if (obs_dim == 7 && act_dim == 2)
+        hipLaunchKernelGGL((policy_act_kernel<7, 2>), grid, block, 0, s, params, n, env_id_offset, obs, lo, hi, iter,
+                           (uint32_t)t, action_env, action, value, log_prob, obs_copy);
+    else
+        return fail(RR_EINVAL, "rr_policy_act: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_policy_act: launch");
+}
+
+int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int64_t n, const float* term_obs,
+                        const uint8_t* truncated, const float* reward, float gamma, float* reward_out, void* stream)
+{
+    if (!params || !term_obs || !truncated || !reward || !reward_out || n <= 0)
+        return fail(RR_EINVAL, "rr_policy_bootstrap: null argument or n <= 0");
+    if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_policy_bootstrap: params must be 16-B aligned");
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock)), block(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    if (obs_dim == 14 && act_dim == 3)
+        hipLaunchKernelGGL((policy_bootstrap_kernel<14, 3>), grid, block, 0, s, params, n, term_obs, truncated,
+                           reward, gamma, reward_out);
+    else if (obs_dim == 7 && act_dim == 2)
+        hipLaunchKernelGGL((policy_bootstrap_kernel<7, 2>), grid, block, 0, s, params, n, term_obs, truncated, reward,
+                           gamma, reward_out);
+    else
+        return fail(RR_EINVAL, "rr_policy_bootstrap: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_policy_bootstrap: launch");
+}
+
+int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, const float* starts,
+           const float* last_value, const float* last_done, float gamma, float lam, float* advantages,
+           float* returns, void* stream)
+{
+    if (!rewards || !values || !starts || !last_value || !last_done || !advantages || !returns || T <= 0 || n <= 0)
+        return fail(RR_EINVAL, "rr_gae: null argument or empty rollout");
+    hipLaunchKernelGGL(gae_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
+                       T, n, rewards, values, starts, last_value, last_done, gamma, lam, advantages, returns);
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_gae: launch");
 }
 
 #if RR_DIAG == 4

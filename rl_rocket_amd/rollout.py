@@ -23,6 +23,7 @@ from torch import nn
 class MlpActorCritic(nn.Module):
     def __init__(self, obs_dim, act_dim, hidden=(64, 64), log_std_init=0.0):
         super().__init__()
+        self.hidden = tuple(hidden)
 
         def mlp():
             layers, d = [], obs_dim
@@ -59,11 +60,86 @@ class MlpActorCritic(nn.Module):
         return (0.5 + 0.5 * math.log(2 * math.pi) + self.log_std).sum().expand(n)
 
 
+class PolicyPack:
+    """Packs an ``MlpActorCritic``'s weights into the fragment-ordered fp32 buffer of the
+    fused HIP policy kernel (layout: rl_rocket_amd/csrc/rocket_policy.inc, offsets from
+    ``rr_policy_layout``). ``pack()`` is pure device tensor work on the live parameters,
+    so it can sit inside a captured graph and always reflects the current weights."""
+
+    def __init__(self, policy, obs_dim, act_dim, device):
+        import ctypes
+
+        from . import _lib
+
+        lib = _lib.load()
+        off = (ctypes.c_int64 * 12)()
+        size = _lib.check(lib.rr_policy_layout(obs_dim, act_dim, off), "rr_policy_layout")
+        self.off = dict(zip(("L1A", "B1", "L2A", "B2", "TOWER", "PI", "VF", "HA", "HV", "HB", "VB", "LS"), list(off)))
+        self.size, self.obs_dim, self.act_dim, self.policy = size, obs_dim, act_dim, policy
+        self.buf = torch.zeros(size + 4, dtype=torch.float32, device=device)  # +4: 16-B alignment slack
+        if self.buf.data_ptr() % 16:
+            raise RuntimeError("packed policy buffer not 16-B aligned")
+        dev = device
+        lane = torch.arange(64, device=dev)
+        r, hh = lane & 31, lane >> 5
+        reg = torch.arange(16, device=dev)
+
+        def row(rg, h):  # D-layout row of register rg in lane half h
+            return (rg & 3) + 8 * (rg >> 2) + 4 * h
+
+        kp1 = (obs_dim + 1) // 2
+        m = torch.arange(2, device=dev)
+        s_ = torch.arange(kp1, device=dev)
+        # L1A[m][s][lane] = W1[32m + r][2s + hh]  (k >= obs_dim -> padded column)
+        k1 = 2 * s_[None, :, None] + hh[None, None, :]
+        self.l1_i = (32 * m[:, None, None] + r[None, None, :]).expand(2, kp1, 64).reshape(-1)
+        self.l1_k = k1.expand(2, kp1, 64).reshape(-1)
+        # B[m][half][reg] = b[32m + row(reg, half)]
+        half = torch.arange(2, device=dev)
+        self.b_i = (32 * m[:, None, None] + row(reg[None, None, :], half[None, :, None])).reshape(-1)
+        # L2A[m][t][g][lane][rr] = W2[32m + r][32t + row(4g + rr, hh)]
+        t = torch.arange(2, device=dev)
+        g = torch.arange(4, device=dev)
+        rr = torch.arange(4, device=dev)
+        shp = (2, 2, 4, 64, 4)
+        self.l2_i = (32 * m.view(2, 1, 1, 1, 1) + r.view(1, 1, 1, 64, 1)).expand(shp).reshape(-1)
+        self.l2_k = (32 * t.view(1, 2, 1, 1, 1) + row(4 * g.view(1, 1, 4, 1, 1) + rr.view(1, 1, 1, 1, 4),
+                                                        hh.view(1, 1, 1, 64, 1))).expand(shp).reshape(-1)
+
+    def _tower(self, net, base):
+        o = self.off
+        w1, b1, w2, b2 = net[0].weight, net[0].bias, net[2].weight, net[2].bias
+        w1p = torch.nn.functional.pad(w1, (0, 1))  # column obs_dim = 0 (odd obs_dim padding)
+        kp1 = (self.obs_dim + 1) // 2
+        self.buf[base + o["L1A"]: base + o["L1A"] + 2 * kp1 * 64] = w1p[self.l1_i, self.l1_k]
+        self.buf[base + o["B1"]: base + o["B1"] + 64] = b1[self.b_i]
+        self.buf[base + o["L2A"]: base + o["L2A"] + 4096] = w2[self.l2_i, self.l2_k]
+        self.buf[base + o["B2"]: base + o["B2"] + 64] = b2[self.b_i]
+
+    @torch.no_grad()
+    def pack(self):
+        p, o, na = self.policy, self.off, self.act_dim
+        self._tower(p.pi_net, o["PI"])
+        self._tower(p.vf_net, o["VF"])
+        self.buf[o["HA"]: o["HA"] + 64 * na] = p.action_net.weight[:, self.b_i].reshape(-1)
+        self.buf[o["HV"]: o["HV"] + 64] = p.value_net.weight[0, self.b_i]
+        self.buf[o["HB"]: o["HB"] + na] = p.action_net.bias
+        self.buf[o["VB"]: o["VB"] + 1] = p.value_net.bias
+        self.buf[o["LS"]: o["LS"] + na] = p.log_std
+        return self.buf
+
+
 class DeviceRollout:
     """Collects ``n_steps`` transitions from a ``RocketBatch`` (auto-reset, TimeLimit)
-    into device tensors [n_steps, N, ...] and computes GAE on device."""
+    into device tensors [n_steps, N, ...] and computes GAE on device.
 
-    def __init__(self, batch, policy, n_steps=16, gamma=0.99, gae_lambda=0.95, generator=None):
+    ``fused=True`` (default for an ``MlpActorCritic`` with 64x64 towers): per step one
+    fp32-MFMA HIP launch for policy forward + sampling + buffer writes (``rr_policy_act``),
+    the fused env step, one launch for the timeout bootstrap (``rr_policy_bootstrap``);
+    GAE in one launch (``rr_gae``). ``fused=False``: the same algorithm in PyTorch ops."""
+
+    def __init__(self, batch, policy, n_steps=16, gamma=0.99, gae_lambda=0.95, generator=None, fused=None,
+                 seed=0):
         self.env, self.policy = batch, policy
         self.n_steps, self.gamma, self.lam = n_steps, gamma, gae_lambda
         n, ns, na = batch.num_envs, batch.state_dim, batch.action_dim
@@ -85,9 +161,31 @@ class DeviceRollout:
         self._clipped = torch.zeros((n, na), **f)
         self._tobs = torch.zeros((n, ns), **f)
         self._r = torch.zeros((n,), **f)
+        if fused is None:
+            fused = isinstance(policy, MlpActorCritic) and policy.hidden == (64, 64) and (ns, na) in ((14, 3), (7, 2))
+        self.fused = bool(fused)
+        if self.fused:
+            from . import _lib
+
+            self._lib = _lib.load()
+            self._pack = PolicyPack(policy, ns, na, dev)
+            self.iter = torch.zeros((1,), dtype=torch.int64, device=dev)  # advanced by every collect (graph-safe)
+            self.seed = int(seed) & (2 ** 64 - 1)
+            self._ones = torch.ones((n,), dtype=torch.uint8, device=dev)
+            self._zeros = torch.zeros((n,), **f)
+            import ctypes
+
+            from .batch import _ptr
+
+            self._c, self._p = ctypes, _ptr
+            bufs = _lib.RrBuffers()
+            _lib.check(self._lib.rr_get_buffers(batch._h, ctypes.byref(bufs)), "rr_get_buffers")
+            self._term_obs = ctypes.c_void_p(bufs.terminal_obs)
 
     @torch.no_grad()
     def collect(self):
+        if self.fused:
+            return self._collect_fused()
         env, pol = self.env, self.policy
         for t in range(self.n_steps):
             obs = self.last_obs
@@ -110,6 +208,34 @@ class DeviceRollout:
         self.last_value.copy_(pol.value(self.last_obs))
         self.last_done.copy_(self.last_start)
         self._gae()
+
+    def _collect_fused(self):
+        env, lib, c, p = self.env, self._lib, self._c, self._p
+        from . import _lib
+
+        n, ns, na = env.num_envs, env.state_dim, env.action_dim
+        params = p(self._pack.pack())
+        stream = c.c_void_p(torch.cuda.current_stream(env.device).cuda_stream)
+        it = p(self.iter)
+        for t in range(self.n_steps):
+            _lib.check(lib.rr_policy_act(params, ns, na, n, env.env_id_offset, p(self.last_obs), self.seed, it, t, p(self._clipped),
+                                         p(self.actions[t]), p(self.values[t]), p(self.log_probs[t]), p(self.obs[t]),
+                                         stream), "rr_policy_act")
+            self.starts[t].copy_(self.last_start)
+            nobs, rew, done, trunc = env.step(self._clipped)
+            # SB3 1.6: reward += gamma * V(terminal_obs) where TimeLimit truncated the episode
+            _lib.check(lib.rr_policy_bootstrap(params, ns, na, n, self._term_obs, p(trunc), p(rew), self.gamma,
+                                               p(self.rewards[t]), stream), "rr_policy_bootstrap")
+            self.last_obs.copy_(nobs)
+            self.last_start.copy_(done)
+        # V(last obs) through the bootstrap kernel: 0 + 1 * V(obs) for every env
+        _lib.check(lib.rr_policy_bootstrap(params, ns, na, n, p(self.last_obs), p(self._ones), p(self._zeros), 1.0,
+                                           p(self.last_value), stream), "rr_policy_bootstrap")
+        self.last_done.copy_(self.last_start)
+        _lib.check(lib.rr_gae(self.n_steps, n, p(self.rewards), p(self.values), p(self.starts), p(self.last_value),
+                              p(self.last_done), self.gamma, self.lam, p(self.advantages), p(self.returns), stream),
+                   "rr_gae")
+        self.iter.add_(1)
 
     def _gae(self):
         """SB3 RolloutBuffer.compute_returns_and_advantage, on device."""

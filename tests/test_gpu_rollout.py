@@ -1,0 +1,144 @@
+"""The fused on-device rollout kernels (rl_rocket_amd/csrc/rocket_policy.inc) against the
+PyTorch restatement of SB3's MlpPolicy / collect_rollouts / GAE (rl_rocket_amd/rollout.py),
+fp32. Tolerances: 2e-5 absolute on policy outputs of O(1) (MFMA fp32 fma chains in another
+order, tanh via exp2/rcp), 1e-5 on GAE."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5
+
+
+def _policy(ns, na, seed=0):
+    import torch
+    from rl_rocket_amd.rollout import MlpActorCritic
+
+    torch.manual_seed(seed)
+    pol = MlpActorCritic(ns, na).cuda()
+    with torch.no_grad():  # move off SB3's small-gain init so every weight matters
+        for prm in pol.parameters():
+            prm.add_(0.3 * torch.randn_like(prm))
+    return pol
+
+
+@pytest.mark.parametrize("ns,na", [(14, 3), (7, 2)])
+def test_policy_act_matches_torch(ns, na):
+    import torch
+    from rl_rocket_amd import _lib
+    from rl_rocket_amd.batch import _ptr
+    from rl_rocket_amd.rollout import PolicyPack
+
+    lib = _lib.load()
+    n = 4096 + 37  # ragged last wave
+    pol = _policy(ns, na)
+    params = PolicyPack(pol, ns, na, torch.device("cuda:0")).pack()
+    obs = torch.randn((n, ns), device="cuda:0") * 2
+    it = torch.tensor([5], dtype=torch.int64, device="cuda:0")
+    act_env, act = torch.empty((n, na), device="cuda:0"), torch.empty((n, na), device="cuda:0")
+    val, lp, ocopy = (torch.empty((n,), device="cuda:0"), torch.empty((n,), device="cuda:0"),
+                      torch.empty((n, ns), device="cuda:0"))
+    _lib.check(lib.rr_policy_act(_ptr(params), ns, na, n, 0, _ptr(obs), 123, _ptr(it), 3, _ptr(act_env), _ptr(act),
+                                 _ptr(val), _ptr(lp), _ptr(ocopy), None), "rr_policy_act")
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        mean, v = pol(obs)
+        std = pol.log_std.exp()
+    print("value err", (val - v).abs().max().item())
+    assert (val - v).abs().max().item() < TOL
+    assert torch.equal(ocopy, obs)
+    assert torch.equal(act_env, act.clamp(-1, 1))
+    eps = (act - mean) / std
+    ref_lp = (-0.5 * eps ** 2 - pol.log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+    assert (lp - ref_lp).abs().max().item() < 1e-4
+    e = eps.cpu().numpy()
+    assert abs(e.mean()) < 0.05 and abs(e.std() - 1) < 0.05  # N(0, 1) draws
+    # determinism and fresh noise per (iter, t)
+    act2 = torch.empty_like(act)
+    _lib.check(lib.rr_policy_act(_ptr(params), ns, na, n, 0, _ptr(obs), 123, _ptr(it), 3, _ptr(act_env), _ptr(act2),
+                                 _ptr(val), _ptr(lp), None, None), "rr_policy_act")
+    it.add_(1)
+    act3 = torch.empty_like(act)
+    _lib.check(lib.rr_policy_act(_ptr(params), ns, na, n, 0, _ptr(obs), 123, _ptr(it), 3, _ptr(act_env), _ptr(act3),
+                                 _ptr(val), _ptr(lp), None, None), "rr_policy_act")
+    torch.cuda.synchronize()
+    assert torch.equal(act, act2)
+    assert not torch.equal(act, act3)
+
+
+def test_policy_bootstrap_and_gae():
+    import torch
+    from rl_rocket_amd import _lib
+    from rl_rocket_amd.batch import _ptr
+    from rl_rocket_amd.rollout import PolicyPack
+
+    lib = _lib.load()
+    n, ns, na = 8192, 14, 3
+    pol = _policy(ns, na, seed=1)
+    params = PolicyPack(pol, ns, na, torch.device("cuda:0")).pack()
+    tobs = torch.randn((n, ns), device="cuda:0")
+    trunc = (torch.rand((n,), device="cuda:0") < 0.01).to(torch.uint8)
+    trunc[:300] = 0  # whole workgroups without a truncation take the copy-only path
+    rew = torch.randn((n,), device="cuda:0")
+    out = torch.empty_like(rew)
+    _lib.check(lib.rr_policy_bootstrap(_ptr(params), ns, na, n, _ptr(tobs), _ptr(trunc), _ptr(rew), 0.99, _ptr(out),
+                                       None), "rr_policy_bootstrap")
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref = rew + 0.99 * pol.value(tobs) * trunc.float()
+    assert (out - ref).abs().max().item() < TOL
+    # GAE kernel vs the PyTorch scan
+    T = 16
+    r, v, s = torch.randn((T, n), device="cuda:0"), torch.randn((T, n), device="cuda:0"), \
+        (torch.rand((T, n), device="cuda:0") < 0.05).float()
+    lv, ld = torch.randn((n,), device="cuda:0"), (torch.rand((n,), device="cuda:0") < 0.05).float()
+    adv, ret = torch.empty_like(r), torch.empty_like(r)
+    _lib.check(lib.rr_gae(T, n, _ptr(r), _ptr(v), _ptr(s), _ptr(lv), _ptr(ld), 0.99, 0.95, _ptr(adv), _ptr(ret), None),
+               "rr_gae")
+    torch.cuda.synchronize()
+    last, ref_adv = torch.zeros(n, device="cuda:0"), torch.empty_like(r)
+    for t in reversed(range(T)):
+        nt = 1.0 - (ld if t == T - 1 else s[t + 1])
+        nv = lv if t == T - 1 else v[t + 1]
+        last = r[t] + 0.99 * nv * nt - v[t] + 0.99 * 0.95 * nt * last
+        ref_adv[t] = last
+    assert (adv - ref_adv).abs().max().item() < 1e-5
+    assert (ret - (ref_adv + v)).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_fused_collect_matches_semantics(fused):
+    """A fused and an unfused rollout of the same policy share every deterministic output
+    (value of each visited obs, buffer layout) and both are graph-capturable."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout
+
+    n, T = 4096, 8
+    env = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=6, **ENV_CONFIG_6DOF)
+    pol = _policy(14, 3, seed=2)
+    ro = DeviceRollout(env, pol, n_steps=T, fused=fused)
+    assert ro.fused == fused
+    ro.collect()
+    with torch.no_grad():
+        v = pol.value(ro.obs.reshape(-1, 14)).reshape(T, n)
+    assert (ro.values - v).abs().max().item() < TOL
+    for tns in (ro.obs, ro.actions, ro.rewards, ro.values, ro.log_probs, ro.advantages, ro.returns):
+        assert torch.isfinite(tns).all()
+    assert ro.starts[1:].sum() > 0  # TimeLimit 6 < T: episodes restart inside the rollout
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(g, stream=st):
+            ro.collect()
+    torch.cuda.current_stream().wait_stream(st)
+    a0 = ro.actions.clone()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.isfinite(ro.rewards).all() and not torch.equal(a0, ro.actions)
+    env.close()
