@@ -189,20 +189,34 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
  * by rl_rocket_amd.rollout.pack_policy). Host-only. */
 int rr_policy_layout(int obs_dim, int act_dim, int64_t* off);
 
-/* Policy forward + Gaussian sample for n envs (SB3 ActorCriticPolicy.forward + clip):
+/* Fill the packed buffer (device, rr_policy_layout floats) from the 13 device fp32 tensors
+ * of the actor-critic in PyTorch nn.Linear layouts ([out][in] row-major), src[] being a
+ * HOST array of device pointers: pi {W1 [64][obs], b1, W2 [64][64], b2}, vf {W1, b1, W2,
+ * b2}, W_action [act][64], b_action, W_value [1][64], b_value, log_std [act]. One launch. */
+int rr_policy_pack(int obs_dim, int act_dim, const float* const* src, float* params, void* stream);
+
+/* One rollout step's policy work (SB3 ActorCriticPolicy.forward + clip, plus the previous
+ * step's bookkeeping of collect_rollouts) in one launch:
  *   obs [n][obs_dim] -> action_env [n][act_dim] (clip to [-1, 1], the rr_step input),
  *   action [n][act_dim] (unclipped sample), value [n], log_prob [n], obs_copy [n][obs_dim]
  *   (or NULL; the rollout buffer's obs[t]). The normal draws are counter-based on
  *   (seed, env_id_offset + i, *iter, t): `iter` is a device uint64 the caller advances once
- *   per rollout, so graph replays draw new noise. params 16-B aligned. */
+ *   per rollout, so graph replays draw new noise. params 16-B aligned.
+ *   If reward_out != NULL: reward_out[i] = prev_reward[i] + gamma * V(prev_term_obs[i])
+ *   where prev_truncated[i] (the timeout bootstrap of step t-1; rr_step's outputs and
+ *   rr_get_buffers' terminal_obs). If start_out != NULL: start_out[i] = done[i] (episode
+ *   start flags of step t). */
 int rr_policy_act(const float* params, int obs_dim, int act_dim, int64_t n, int64_t env_id_offset, const float* obs,
                   uint64_t seed, const uint64_t* iter, int t, float* action_env, float* action, float* value,
-                  float* log_prob, float* obs_copy, void* stream);
+                  float* log_prob, float* obs_copy, const float* prev_term_obs, const uint8_t* prev_truncated,
+                  const float* prev_reward, float gamma, float* reward_out, const uint8_t* done, float* start_out,
+                  void* stream);
 
-/* Timeout bootstrap of collect_rollouts: reward_out[i] = reward[i] + gamma * V(term_obs[i])
- * where truncated[i] (TimeLimit.truncated), else reward[i]. */
+/* End of a rollout: reward_out[i] = reward[i] + gamma * V(term_obs[i]) where truncated[i]
+ * (TimeLimit.truncated), else reward[i]; and, if value_out != NULL, value_out[i] = V(obs[i]). */
 int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int64_t n, const float* term_obs,
-                        const uint8_t* truncated, const float* reward, float gamma, float* reward_out, void* stream);
+                        const uint8_t* truncated, const float* reward, float gamma, float* reward_out,
+                        const float* obs, float* value_out, void* stream);
 
 /* RolloutBuffer.compute_returns_and_advantage: rewards / values / starts [T][n] (starts[t]
  * = episode-start flag of step t), last_value / last_done [n] -> advantages, returns [T][n]. */

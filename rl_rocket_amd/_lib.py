@@ -99,10 +99,12 @@ SIGNATURES = {
     "rr_fetch_done": (ctypes.c_int64, [_P, ctypes.c_int64, _P, _P, _P, _P, _P]),
     "rr_copy_terminal": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_policy_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P]),
+    "rr_policy_pack": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P, _P]),
     "rr_policy_act": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_uint64,
-                                     _P, ctypes.c_int, _P, _P, _P, _P, _P, _P]),
+                                     _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P,
+                                     _P]),
     "rr_policy_bootstrap": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _P, _P, _P, ctypes.c_float,
-                                           _P, _P]),
+                                           _P, _P, _P, _P]),
     "rr_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, _P,
                               _P, _P]),
 }

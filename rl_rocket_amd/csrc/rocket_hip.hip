@@ -1631,22 +1631,51 @@ int rr_policy_layout(int obs_dim, int act_dim, int64_t* off)
     return fail(RR_EINVAL, "rr_policy_layout: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
 }
 
+int rr_policy_pack(int obs_dim, int act_dim, const float* const* src, float* params, void* stream)
+{
+    if (!src || !params) return fail(RR_EINVAL, "rr_policy_pack: null argument");
+    PolSrc ps;
+    for (int k = 0; k < 13; ++k) {
+        if (!src[k]) return fail(RR_EINVAL, "rr_policy_pack: null parameter tensor");
+        ps.p[k] = src[k];
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (obs_dim == 14 && act_dim == 3) {
+        using L = pol::Layout<14, 3>;
+        hipLaunchKernelGGL((policy_pack_kernel<14, 3>), dim3((L::SIZE + 255) / 256), dim3(256), 0, s, ps, params);
+    } else if (obs_dim == 7 && act_dim == 2) {
+        using L = pol::Layout<7, 2>;
+        hipLaunchKernelGGL((policy_pack_kernel<7, 2>), dim3((L::SIZE + 255) / 256), dim3(256), 0, s, ps, params);
+    } else {
+        return fail(RR_EINVAL, "rr_policy_pack: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+    }
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_policy_pack: launch");
+}
+
 int rr_policy_act(const float* params, int obs_dim, int act_dim, int64_t n, int64_t env_id_offset, const float* obs,
                   uint64_t seed, const uint64_t* iter, int t, float* action_env, float* action, float* value,
-                  float* log_prob, float* obs_copy, void* stream)
+                  float* log_prob, float* obs_copy, const float* prev_term_obs, const uint8_t* prev_truncated,
+                  const float* prev_reward, float gamma, float* reward_out, const uint8_t* done, float* start_out,
+                  void* stream)
 {
     if (!params || !obs || !iter || !action_env || !action || !value || !log_prob || n <= 0)
         return fail(RR_EINVAL, "rr_policy_act: null argument or n <= 0");
+    if (reward_out && (!prev_term_obs || !prev_truncated || !prev_reward))
+        return fail(RR_EINVAL, "rr_policy_act: reward_out needs prev_term_obs, prev_truncated, prev_reward");
+    if (start_out && !done) return fail(RR_EINVAL, "rr_policy_act: start_out needs done");
     if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_policy_act: params must be 16-B aligned");
-    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock)), block(kBlock);
+    const dim3 grid((unsigned)((n + pol::kEnvsPerBlock - 1) / pol::kEnvsPerBlock)), block(pol::kThreads);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
     if (obs_dim == 14 && act_dim == 3)
         hipLaunchKernelGGL((policy_act_kernel<14, 3>), grid, block, 0, s, params, n, env_id_offset, obs, lo, hi, iter,
-                           (uint32_t)t, action_env, action, value, log_prob, obs_copy);
+                           (uint32_t)t, action_env, action, value, log_prob, obs_copy, prev_term_obs, prev_truncated,
+                           prev_reward, gamma, reward_out, done, start_out);
     else if (obs_dim == 7 && act_dim == 2)
         hipLaunchKernelGGL((policy_act_kernel<7, 2>), grid, block, 0, s, params, n, env_id_offset, obs, lo, hi, iter,
-                           (uint32_t)t, action_env, action, value, log_prob, obs_copy);
+                           (uint32_t)t, action_env, action, value, log_prob, obs_copy, prev_term_obs, prev_truncated,
+                           prev_reward, gamma, reward_out, done, start_out);
     else
         return fail(RR_EINVAL, "rr_policy_act: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
     hipError_t err = hipGetLastError();
@@ -1654,19 +1683,21 @@ int rr_policy_act(const float* params, int obs_dim, int act_dim, int64_t n, int6
 }
 
 int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int64_t n, const float* term_obs,
-                        const uint8_t* truncated, const float* reward, float gamma, float* reward_out, void* stream)
+                        const uint8_t* truncated, const float* reward, float gamma, float* reward_out,
+                        const float* obs, float* value_out, void* stream)
 {
     if (!params || !term_obs || !truncated || !reward || !reward_out || n <= 0)
         return fail(RR_EINVAL, "rr_policy_bootstrap: null argument or n <= 0");
+    if (value_out && !obs) return fail(RR_EINVAL, "rr_policy_bootstrap: value_out needs obs");
     if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_policy_bootstrap: params must be 16-B aligned");
-    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock)), block(kBlock);
+    const dim3 grid((unsigned)((n + pol::kEnvsPerBlock - 1) / pol::kEnvsPerBlock)), block(pol::kThreads);
     hipStream_t s = (hipStream_t)stream;
     if (obs_dim == 14 && act_dim == 3)
         hipLaunchKernelGGL((policy_bootstrap_kernel<14, 3>), grid, block, 0, s, params, n, term_obs, truncated,
-                           reward, gamma, reward_out);
+                           reward, gamma, reward_out, obs, value_out);
     else if (obs_dim == 7 && act_dim == 2)
         hipLaunchKernelGGL((policy_bootstrap_kernel<7, 2>), grid, block, 0, s, params, n, term_obs, truncated, reward,
-                           gamma, reward_out);
+                           gamma, reward_out, obs, value_out);
     else
         return fail(RR_EINVAL, "rr_policy_bootstrap: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
     hipError_t err = hipGetLastError();

@@ -116,8 +116,33 @@ class PolicyPack:
         self.buf[base + o["L2A"]: base + o["L2A"] + 4096] = w2[self.l2_i, self.l2_k]
         self.buf[base + o["B2"]: base + o["B2"] + 64] = b2[self.b_i]
 
+    def _sources(self):
+        p = self.policy
+        ts = [p.pi_net[0].weight, p.pi_net[0].bias, p.pi_net[2].weight, p.pi_net[2].bias,
+              p.vf_net[0].weight, p.vf_net[0].bias, p.vf_net[2].weight, p.vf_net[2].bias,
+              p.action_net.weight, p.action_net.bias, p.value_net.weight, p.value_net.bias, p.log_std]
+        for t in ts:
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.buf.device:
+                raise ValueError("rr_policy_pack needs contiguous fp32 parameters on the rollout device")
+        return ts
+
     @torch.no_grad()
     def pack(self):
+        """One HIP launch (rr_policy_pack) from the live parameter tensors."""
+        import ctypes
+
+        from . import _lib
+
+        ts = self._sources()
+        src = (ctypes.c_void_p * 13)(*[t.data_ptr() for t in ts])
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.buf.device).cuda_stream)
+        _lib.check(_lib.load().rr_policy_pack(self.obs_dim, self.act_dim, src, ctypes.c_void_p(self.buf.data_ptr()),
+                                              stream), "rr_policy_pack")
+        return self.buf
+
+    @torch.no_grad()
+    def pack_reference(self):
+        """The same layout with PyTorch index ops (test reference for rr_policy_pack)."""
         p, o, na = self.policy, self.off, self.act_dim
         self._tower(p.pi_net, o["PI"])
         self._tower(p.vf_net, o["VF"])
@@ -181,6 +206,7 @@ class DeviceRollout:
             bufs = _lib.RrBuffers()
             _lib.check(self._lib.rr_get_buffers(batch._h, ctypes.byref(bufs)), "rr_get_buffers")
             self._term_obs = ctypes.c_void_p(bufs.terminal_obs)
+            batch.done.fill_(1)  # SB3: _last_episode_starts = ones before the first rollout
 
     @torch.no_grad()
     def collect(self):
@@ -210,28 +236,30 @@ class DeviceRollout:
         self._gae()
 
     def _collect_fused(self):
+        """Two launches per step: rr_policy_act (forward + sample of step t, bootstrap of
+        step t-1, episode-start flags) and the fused env step; obs are read in place from
+        the env's output buffer."""
         env, lib, c, p = self.env, self._lib, self._c, self._p
         from . import _lib
 
         n, ns, na = env.num_envs, env.state_dim, env.action_dim
         params = p(self._pack.pack())
         stream = c.c_void_p(torch.cuda.current_stream(env.device).cuda_stream)
-        it = p(self.iter)
+        it, obs, done = p(self.iter), p(env.obs), p(env.done)
         for t in range(self.n_steps):
-            _lib.check(lib.rr_policy_act(params, ns, na, n, env.env_id_offset, p(self.last_obs), self.seed, it, t, p(self._clipped),
+            prev = t > 0
+            _lib.check(lib.rr_policy_act(params, ns, na, n, env.env_id_offset, obs, self.seed, it, t, p(self._clipped),
                                          p(self.actions[t]), p(self.values[t]), p(self.log_probs[t]), p(self.obs[t]),
-                                         stream), "rr_policy_act")
-            self.starts[t].copy_(self.last_start)
-            nobs, rew, done, trunc = env.step(self._clipped)
-            # SB3 1.6: reward += gamma * V(terminal_obs) where TimeLimit truncated the episode
-            _lib.check(lib.rr_policy_bootstrap(params, ns, na, n, self._term_obs, p(trunc), p(rew), self.gamma,
-                                               p(self.rewards[t]), stream), "rr_policy_bootstrap")
-            self.last_obs.copy_(nobs)
-            self.last_start.copy_(done)
-        # V(last obs) through the bootstrap kernel: 0 + 1 * V(obs) for every env
-        _lib.check(lib.rr_policy_bootstrap(params, ns, na, n, p(self.last_obs), p(self._ones), p(self._zeros), 1.0,
-                                           p(self.last_value), stream), "rr_policy_bootstrap")
-        self.last_done.copy_(self.last_start)
+                                         self._term_obs if prev else None, p(env.truncated) if prev else None,
+                                         p(env.reward) if prev else None, self.gamma,
+                                         p(self.rewards[t - 1]) if prev else None, done, p(self.starts[t]), stream),
+                       "rr_policy_act")
+            env.step(self._clipped)
+        _lib.check(lib.rr_policy_bootstrap(params, ns, na, n, self._term_obs, p(env.truncated), p(env.reward),
+                                           self.gamma, p(self.rewards[self.n_steps - 1]), obs, p(self.last_value),
+                                           stream), "rr_policy_bootstrap")
+        self.last_done.copy_(env.done)
+        self.last_start.copy_(env.done)
         _lib.check(lib.rr_gae(self.n_steps, n, p(self.rewards), p(self.values), p(self.starts), p(self.last_value),
                               p(self.last_done), self.gamma, self.lam, p(self.advantages), p(self.returns), stream),
                    "rr_gae")

@@ -42,7 +42,8 @@ def test_policy_act_matches_torch(ns, na):
     val, lp, ocopy = (torch.empty((n,), device="cuda:0"), torch.empty((n,), device="cuda:0"),
                       torch.empty((n, ns), device="cuda:0"))
     _lib.check(lib.rr_policy_act(_ptr(params), ns, na, n, 0, _ptr(obs), 123, _ptr(it), 3, _ptr(act_env), _ptr(act),
-                                 _ptr(val), _ptr(lp), _ptr(ocopy), None), "rr_policy_act")
+                                 _ptr(val), _ptr(lp), _ptr(ocopy), None, None, None, 0.0, None, None, None, None),
+               "rr_policy_act")
     torch.cuda.synchronize()
     with torch.no_grad():
         mean, v = pol(obs)
@@ -59,14 +60,29 @@ def test_policy_act_matches_torch(ns, na):
     # determinism and fresh noise per (iter, t)
     act2 = torch.empty_like(act)
     _lib.check(lib.rr_policy_act(_ptr(params), ns, na, n, 0, _ptr(obs), 123, _ptr(it), 3, _ptr(act_env), _ptr(act2),
-                                 _ptr(val), _ptr(lp), None, None), "rr_policy_act")
+                                 _ptr(val), _ptr(lp), None, None, None, None, 0.0, None, None, None, None),
+               "rr_policy_act")
     it.add_(1)
     act3 = torch.empty_like(act)
     _lib.check(lib.rr_policy_act(_ptr(params), ns, na, n, 0, _ptr(obs), 123, _ptr(it), 3, _ptr(act_env), _ptr(act3),
-                                 _ptr(val), _ptr(lp), None, None), "rr_policy_act")
+                                 _ptr(val), _ptr(lp), None, None, None, None, 0.0, None, None, None, None),
+               "rr_policy_act")
     torch.cuda.synchronize()
     assert torch.equal(act, act2)
     assert not torch.equal(act, act3)
+
+
+@pytest.mark.parametrize("ns,na", [(14, 3), (7, 2)])
+def test_policy_pack_kernel_matches_reference(ns, na):
+    import torch
+    from rl_rocket_amd.rollout import PolicyPack
+
+    pk = PolicyPack(_policy(ns, na, seed=4), ns, na, torch.device("cuda:0"))
+    ref = pk.pack_reference().clone()
+    pk.buf.fill_(float("nan"))
+    out = pk.pack()
+    torch.cuda.synchronize()
+    assert torch.equal(out[:pk.size], ref[:pk.size])
 
 
 def test_policy_bootstrap_and_gae():
@@ -84,12 +100,28 @@ def test_policy_bootstrap_and_gae():
     trunc[:300] = 0  # whole workgroups without a truncation take the copy-only path
     rew = torch.randn((n,), device="cuda:0")
     out = torch.empty_like(rew)
+    obs = torch.randn((n, ns), device="cuda:0")
+    vout = torch.empty_like(rew)
     _lib.check(lib.rr_policy_bootstrap(_ptr(params), ns, na, n, _ptr(tobs), _ptr(trunc), _ptr(rew), 0.99, _ptr(out),
-                                       None), "rr_policy_bootstrap")
+                                       _ptr(obs), _ptr(vout), None), "rr_policy_bootstrap")
     torch.cuda.synchronize()
     with torch.no_grad():
         ref = rew + 0.99 * pol.value(tobs) * trunc.float()
+        vref = pol.value(obs)
     assert (out - ref).abs().max().item() < TOL
+    assert (vout - vref).abs().max().item() < TOL
+    # the same bootstrap fused into rr_policy_act (step t's launch does step t-1's)
+    act_env, act = torch.empty((n, na), device="cuda:0"), torch.empty((n, na), device="cuda:0")
+    val, lp, out2, st = (torch.empty((n,), device="cuda:0") for _ in range(4))
+    done = (torch.rand((n,), device="cuda:0") < 0.1).to(torch.uint8)
+    it = torch.zeros((1,), dtype=torch.int64, device="cuda:0")
+    _lib.check(lib.rr_policy_act(_ptr(params), ns, na, n, 0, _ptr(obs), 1, _ptr(it), 0, _ptr(act_env), _ptr(act),
+                                 _ptr(val), _ptr(lp), None, _ptr(tobs), _ptr(trunc), _ptr(rew), 0.99, _ptr(out2),
+                                 _ptr(done), _ptr(st), None), "rr_policy_act")
+    torch.cuda.synchronize()
+    assert (out2 - ref).abs().max().item() < TOL
+    assert torch.equal(st, done.float())
+    assert (val - vref).abs().max().item() < TOL
     # GAE kernel vs the PyTorch scan
     T = 16
     r, v, s = torch.randn((T, n), device="cuda:0"), torch.randn((T, n), device="cuda:0"), \
