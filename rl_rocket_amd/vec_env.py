@@ -209,3 +209,28 @@ class RocketVecEnv(_VecEnvBase):
     @property
     def unwrapped(self):
         return self
+
+
+class RocketVectorEnv(RocketVecEnv):
+    """The same batched env with the ``gym.vector.VectorEnv`` (gym 0.21) surface the north
+    star names: ``observation_space`` / ``action_space`` are the BATCHED Boxes
+    (num_envs, dim) and ``single_observation_space`` / ``single_action_space`` the per-env
+    ones; ``reset() -> obs``, ``step(actions) -> (obs, rewards, dones, infos)`` with auto-reset
+    and ``infos[i]["terminal_observation"]`` for done envs (SyncVectorEnv semantics);
+    ``reset_async`` / ``reset_wait`` / ``step_async`` / ``step_wait`` / ``close`` / ``seed``.
+    Stepping is the same fused kernel as ``RocketVecEnv``."""
+
+    def __init__(self, num_envs, model="6DOF", **kwargs):
+        super().__init__(num_envs, model=model, **kwargs)
+        ns, na = self.batch.state_dim, self.batch.action_dim
+        self.single_observation_space = self.observation_space
+        self.single_action_space = self.action_space
+        self.observation_space = Box(low=-1, high=1, shape=(self.num_envs, ns)).to_gym()
+        self.action_space = Box(low=-1, high=1, shape=(self.num_envs, na)).to_gym()
+        self.is_vector_env = True
+
+    def reset_async(self):
+        pass
+
+    def reset_wait(self, **kwargs):
+        return self.reset()

@@ -213,3 +213,24 @@ def test_reset_distribution(model):
         assert abs(np.corrcoef(s1[j], s2[j])[0, 1]) < 0.01
     if model == 6:
         assert np.abs(np.linalg.norm(s1[6:10], axis=0) - 1).max() < 1e-5
+
+
+def test_gym_vector_surface():
+    """RocketVectorEnv: gym.vector.VectorEnv naming (batched spaces + single_* spaces),
+    SyncVectorEnv auto-reset semantics with terminal_observation."""
+    from rl_rocket_amd import RocketVectorEnv
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+
+    n = 1024
+    env = RocketVectorEnv(n, model="6DOF", max_episode_steps=5, **ENV_CONFIG_6DOF)
+    assert env.observation_space.shape == (n, 14) and env.single_observation_space.shape == (14,)
+    assert env.action_space.shape == (n, 3) and env.single_action_space.shape == (3,)
+    env.reset_async()
+    obs = env.reset_wait()
+    assert obs.shape == (n, 14)
+    for k in range(5):
+        obs, rew, done, infos = env.step(np.zeros((n, 3), np.float32))
+    assert done.all()  # TimeLimit 5
+    assert len(infos) == n and all("terminal_observation" in infos[i] for i in range(0, n, 97))
+    assert all(infos[i]["TimeLimit.truncated"] in (True, False) for i in range(0, n, 97))
+    env.close()
