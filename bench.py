@@ -45,6 +45,9 @@ def parse():
                     help="step: the fused env step (headline); rollout: on-device PPO rollout "
                          "collection (MlpPolicy 64x64 forward + sample + env step + buffer), BASELINE configs[4]")
     ap.add_argument("--rollout-steps", type=int, default=16)
+    ap.add_argument("--policy-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="rollout mode: fused policy towers on fp32 MFMA (SB3-exact, default) or bf16 MFMA "
+                         "with fp32 accumulation (opt-in)")
     ap.add_argument("--rollout-torch", action="store_true",
                     help="rollout policy / bootstrap / GAE as PyTorch ops instead of the fused HIP kernels")
     return ap.parse_args()
@@ -64,7 +67,8 @@ def bench_rollout(args, dev, n, model, kw):
     env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
                       episode_stats=False, integrator=args.integrator, **kw)
     pol = MlpActorCritic(env.state_dim, env.action_dim).to(dev)
-    ro = DeviceRollout(env, pol, n_steps=args.rollout_steps, fused=not args.rollout_torch)
+    ro = DeviceRollout(env, pol, n_steps=args.rollout_steps, fused=not args.rollout_torch,
+                       policy_dtype=args.policy_dtype)
     for _ in range(3):
         ro.collect()
     torch.cuda.synchronize(dev)
@@ -99,11 +103,13 @@ def bench_rollout(args, dev, n, model, kw):
                   % ("6DOF" if model == 6 else "3DOF", n),
         "value": n * steps / dt, "unit": "env-steps/s", "n_gpus": 1, "steps": steps, "warmup": 3 * args.rollout_steps,
         "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32", "data": "synthetic ICs (env_config init_space), actions from a random-init MlpPolicy",
+        "dtype": "fp32" if args.policy_dtype == "fp32" else "fp32 env, bf16-MFMA policy towers (fp32 accumulate)",
+        "data": "synthetic ICs (env_config init_space), actions from a random-init MlpPolicy",
         "config": {"workload": "Rocket6DOF N=%d, MlpPolicy(64x64 tanh) forward + Gaussian sample + fused step "
                                "+ timeout bootstrap + rollout buffer + GAE, n_steps=%d per hipGraph"
                                % (n, args.rollout_steps), "envs_per_gpu": n,
-                   "policy_path": "PyTorch ops" if args.rollout_torch else "fused HIP (fp32 MFMA) rr_policy_act"},
+                   "policy_path": "PyTorch ops" if args.rollout_torch else
+                   "fused HIP (%s MFMA) rr_policy_act" % args.policy_dtype},
         "gpu_ms_per_collect": e0.elapsed_time(e1) / reps,
         "ppo_epoch_ms": upd * 1e3, "ppo_stats": stats,
     }

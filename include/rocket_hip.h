@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 2
+#define RR_ABI_VERSION 3
 
 /* error codes */
 #define RR_OK 0
@@ -181,19 +181,25 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
  * + RolloutBuffer (the reference trains PPO("MlpPolicy", ...), main_6DOF.py:110-116) for
  * an on-device rollout: the MlpPolicy actor-critic (separate pi / vf towers, net_arch
  * [64, 64], tanh, state-independent log_std) runs as one fp32 MFMA launch per step.
- * Supported (obs_dim, act_dim): (14, 3) 6DOF, (7, 2) 3DOF. */
+ * Supported (obs_dim, act_dim): (14, 3) 6DOF, (7, 2) 3DOF.
+ * precision: RR_POLICY_FP32 (default; v_mfma_f32_32x32x2_f32, exact fp32 products, the
+ * SB3 policy's numbers to fp32 rounding) or RR_POLICY_BF16 (opt-in; v_mfma_f32_32x32x16_bf16
+ * with fp32 accumulation: obs, the tower weights and the first hidden layer rounded to
+ * bf16, everything else fp32). A packed buffer is specific to its precision. */
+#define RR_POLICY_FP32 0
+#define RR_POLICY_BF16 1
 
 /* Packed parameter buffer for rr_policy_*: returns its size in floats (or RR_EINVAL) and,
  * if off != NULL, the 12 section offsets {L1A, B1, L2A, B2, TOWER, PI, VF, HA, HV, HB, VB,
  * LS} (fragment-ordered layout, rl_rocket_amd/csrc/rocket_policy.inc; filled on the device
  * by rl_rocket_amd.rollout.pack_policy). Host-only. */
-int rr_policy_layout(int obs_dim, int act_dim, int64_t* off);
+int rr_policy_layout(int obs_dim, int act_dim, int precision, int64_t* off);
 
 /* Fill the packed buffer (device, rr_policy_layout floats) from the 13 device fp32 tensors
  * of the actor-critic in PyTorch nn.Linear layouts ([out][in] row-major), src[] being a
  * HOST array of device pointers: pi {W1 [64][obs], b1, W2 [64][64], b2}, vf {W1, b1, W2,
  * b2}, W_action [act][64], b_action, W_value [1][64], b_value, log_std [act]. One launch. */
-int rr_policy_pack(int obs_dim, int act_dim, const float* const* src, float* params, void* stream);
+int rr_policy_pack(int obs_dim, int act_dim, int precision, const float* const* src, float* params, void* stream);
 
 /* One rollout step's policy work (SB3 ActorCriticPolicy.forward + clip, plus the previous
  * step's bookkeeping of collect_rollouts) in one launch:
@@ -206,17 +212,17 @@ int rr_policy_pack(int obs_dim, int act_dim, const float* const* src, float* par
  *   where prev_truncated[i] (the timeout bootstrap of step t-1; rr_step's outputs and
  *   rr_get_buffers' terminal_obs). If start_out != NULL: start_out[i] = done[i] (episode
  *   start flags of step t). */
-int rr_policy_act(const float* params, int obs_dim, int act_dim, int64_t n, int64_t env_id_offset, const float* obs,
-                  uint64_t seed, const uint64_t* iter, int t, float* action_env, float* action, float* value,
-                  float* log_prob, float* obs_copy, const float* prev_term_obs, const uint8_t* prev_truncated,
-                  const float* prev_reward, float gamma, float* reward_out, const uint8_t* done, float* start_out,
-                  void* stream);
+int rr_policy_act(const float* params, int obs_dim, int act_dim, int precision, int64_t n, int64_t env_id_offset,
+                  const float* obs, uint64_t seed, const uint64_t* iter, int t, float* action_env, float* action,
+                  float* value, float* log_prob, float* obs_copy, const float* prev_term_obs,
+                  const uint8_t* prev_truncated, const float* prev_reward, float gamma, float* reward_out,
+                  const uint8_t* done, float* start_out, void* stream);
 
 /* End of a rollout: reward_out[i] = reward[i] + gamma * V(term_obs[i]) where truncated[i]
  * (TimeLimit.truncated), else reward[i]; and, if value_out != NULL, value_out[i] = V(obs[i]). */
-int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int64_t n, const float* term_obs,
-                        const uint8_t* truncated, const float* reward, float gamma, float* reward_out,
-                        const float* obs, float* value_out, void* stream);
+int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int precision, int64_t n,
+                        const float* term_obs, const uint8_t* truncated, const float* reward, float gamma,
+                        float* reward_out, const float* obs, float* value_out, void* stream);
 
 /* RolloutBuffer.compute_returns_and_advantage: rewards / values / starts [T][n] (starts[t]
  * = episode-start flag of step t), last_value / last_done [n] -> advantages, returns [T][n]. */

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
@@ -24,6 +24,7 @@ RR_FLAG_REWARD_ANNEALING = 0x4
 RR_FLAG_ACTION_SOA = 0x8
 RR_FLAG_SCIPY_H0_CLAMP = 0x10
 RR_MAX_STATE = 14
+RR_POLICY_FP32, RR_POLICY_BF16 = 0, 1
 
 _d3 = ctypes.c_double * 3
 _f14 = ctypes.c_float * RR_MAX_STATE
@@ -98,13 +99,13 @@ SIGNATURES = {
     "rr_get_buffers": (ctypes.c_int, [_P, ctypes.POINTER(RrBuffers)]),
     "rr_fetch_done": (ctypes.c_int64, [_P, ctypes.c_int64, _P, _P, _P, _P, _P]),
     "rr_copy_terminal": (ctypes.c_int, [_P, _P, _P, _P, _P]),
-    "rr_policy_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P]),
-    "rr_policy_pack": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P, _P]),
-    "rr_policy_act": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_uint64,
-                                     _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P,
-                                     _P]),
-    "rr_policy_bootstrap": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _P, _P, _P, ctypes.c_float,
-                                           _P, _P, _P, _P]),
+    "rr_policy_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
+    "rr_policy_pack": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P]),
+    "rr_policy_act": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, _P,
+                                     ctypes.c_uint64, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P,
+                                     ctypes.c_float, _P, _P, _P, _P]),
+    "rr_policy_bootstrap": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _P, _P, _P,
+                                           ctypes.c_float, _P, _P, _P, _P]),
     "rr_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, _P,
                               _P, _P]),
 }

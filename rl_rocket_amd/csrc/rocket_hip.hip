@@ -1615,23 +1615,54 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
 
 // ---- on-device PPO rollout (rocket_policy.inc) ----
 
-int rr_policy_layout(int obs_dim, int act_dim, int64_t* off)
+}  // extern "C"
+
+template <int O, int A, int P>
+struct PolCfg {
+    static constexpr int OBS = O, ACT = A, PREC = P;
+    using L = pol::Layout<O, A, P>;
+};
+
+// f(PolCfg<...>{}) for a supported (obs_dim, act_dim, precision); false otherwise
+template <class F>
+static bool pol_dispatch(int obs_dim, int act_dim, int precision, F&& f)
 {
-    auto fill = [&](auto L) {
-        using LL = decltype(L);
+    if (precision != RR_POLICY_FP32 && precision != RR_POLICY_BF16) return false;
+    const bool bf = precision == RR_POLICY_BF16;
+    if (obs_dim == 14 && act_dim == 3) {
+        if (bf) f(PolCfg<14, 3, 1>{});
+        else f(PolCfg<14, 3, 0>{});
+        return true;
+    }
+    if (obs_dim == 7 && act_dim == 2) {
+        if (bf) f(PolCfg<7, 2, 1>{});
+        else f(PolCfg<7, 2, 0>{});
+        return true;
+    }
+    return false;
+}
+
+#define RR_POL_UNSUPPORTED(fn) \
+    fail(RR_EINVAL, fn ": supported (obs_dim, act_dim) are (14, 3) and (7, 2), precision RR_POLICY_FP32 / RR_POLICY_BF16")
+
+extern "C" {
+
+int rr_policy_layout(int obs_dim, int act_dim, int precision, int64_t* off)
+{
+    int size = 0;
+    const bool ok = pol_dispatch(obs_dim, act_dim, precision, [&](auto c) {
+        using LL = typename decltype(c)::L;
         if (off) {
             const int64_t v[12] = {LL::L1A, LL::B1, LL::L2A, LL::B2, LL::TOWER, LL::PI,
                                    LL::VF,  LL::HA, LL::HV,  LL::HB, LL::VB,    LL::LS};
             for (int k = 0; k < 12; ++k) off[k] = v[k];
         }
-        return (int)LL::SIZE;
-    };
-    if (obs_dim == 14 && act_dim == 3) return fill(pol::Layout<14, 3>{});
-    if (obs_dim == 7 && act_dim == 2) return fill(pol::Layout<7, 2>{});
-    return fail(RR_EINVAL, "rr_policy_layout: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+        size = LL::SIZE;
+    });
+    return ok ? size : RR_POL_UNSUPPORTED("rr_policy_layout");
 }
 
-int rr_policy_pack(int obs_dim, int act_dim, const float* const* src, float* params, void* stream)
+int rr_policy_pack(int obs_dim, int act_dim, int precision, const float* const* src, float* params, void* stream)
 {
     if (!src || !params) return fail(RR_EINVAL, "rr_policy_pack: null argument");
     PolSrc ps;
@@ -1640,24 +1671,21 @@ int rr_policy_pack(int obs_dim, int act_dim, const float* const* src, float* par
         ps.p[k] = src[k];
     }
     hipStream_t s = (hipStream_t)stream;
-    if (obs_dim == 14 && act_dim == 3) {
-        using L = pol::Layout<14, 3>;
-        hipLaunchKernelGGL((policy_pack_kernel<14, 3>), dim3((L::SIZE + 255) / 256), dim3(256), 0, s, ps, params);
-    } else if (obs_dim == 7 && act_dim == 2) {
-        using L = pol::Layout<7, 2>;
-        hipLaunchKernelGGL((policy_pack_kernel<7, 2>), dim3((L::SIZE + 255) / 256), dim3(256), 0, s, ps, params);
-    } else {
-        return fail(RR_EINVAL, "rr_policy_pack: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
-    }
+    const bool ok = pol_dispatch(obs_dim, act_dim, precision, [&](auto c) {
+        using C = decltype(c);
+        hipLaunchKernelGGL((policy_pack_kernel<C::OBS, C::ACT, C::PREC>), dim3((C::L::SIZE + 255) / 256), dim3(256),
+                           0, s, ps, params);
+    });
+    if (!ok) return RR_POL_UNSUPPORTED("rr_policy_pack");
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_policy_pack: launch");
 }
 
-int rr_policy_act(const float* params, int obs_dim, int act_dim, int64_t n, int64_t env_id_offset, const float* obs,
-                  uint64_t seed, const uint64_t* iter, int t, float* action_env, float* action, float* value,
-                  float* log_prob, float* obs_copy, const float* prev_term_obs, const uint8_t* prev_truncated,
-                  const float* prev_reward, float gamma, float* reward_out, const uint8_t* done, float* start_out,
-                  void* stream)
+int rr_policy_act(const float* params, int obs_dim, int act_dim, int precision, int64_t n, int64_t env_id_offset,
+                  const float* obs, uint64_t seed, const uint64_t* iter, int t, float* action_env, float* action,
+                  float* value, float* log_prob, float* obs_copy, const float* prev_term_obs,
+                  const uint8_t* prev_truncated, const float* prev_reward, float gamma, float* reward_out,
+                  const uint8_t* done, float* start_out, void* stream)
 {
     if (!params || !obs || !iter || !action_env || !action || !value || !log_prob || n <= 0)
         return fail(RR_EINVAL, "rr_policy_act: null argument or n <= 0");
@@ -1668,23 +1696,20 @@ int rr_policy_act(const float* params, int obs_dim, int act_dim, int64_t n, int6
     const dim3 grid((unsigned)((n + pol::kEnvsPerBlock - 1) / pol::kEnvsPerBlock)), block(pol::kThreads);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
-    if (obs_dim == 14 && act_dim == 3)
-        hipLaunchKernelGGL((policy_act_kernel<14, 3>), grid, block, 0, s, params, n, env_id_offset, obs, lo, hi, iter,
-                           (uint32_t)t, action_env, action, value, log_prob, obs_copy, prev_term_obs, prev_truncated,
-                           prev_reward, gamma, reward_out, done, start_out);
-    else if (obs_dim == 7 && act_dim == 2)
-        hipLaunchKernelGGL((policy_act_kernel<7, 2>), grid, block, 0, s, params, n, env_id_offset, obs, lo, hi, iter,
-                           (uint32_t)t, action_env, action, value, log_prob, obs_copy, prev_term_obs, prev_truncated,
-                           prev_reward, gamma, reward_out, done, start_out);
-    else
-        return fail(RR_EINVAL, "rr_policy_act: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+    const bool ok = pol_dispatch(obs_dim, act_dim, precision, [&](auto c) {
+        using C = decltype(c);
+        hipLaunchKernelGGL((policy_act_kernel<C::OBS, C::ACT, C::PREC>), grid, block, 0, s, params, n, env_id_offset,
+                           obs, lo, hi, iter, (uint32_t)t, action_env, action, value, log_prob, obs_copy,
+                           prev_term_obs, prev_truncated, prev_reward, gamma, reward_out, done, start_out);
+    });
+    if (!ok) return RR_POL_UNSUPPORTED("rr_policy_act");
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_policy_act: launch");
 }
 
-int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int64_t n, const float* term_obs,
-                        const uint8_t* truncated, const float* reward, float gamma, float* reward_out,
-                        const float* obs, float* value_out, void* stream)
+int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int precision, int64_t n,
+                        const float* term_obs, const uint8_t* truncated, const float* reward, float gamma,
+                        float* reward_out, const float* obs, float* value_out, void* stream)
 {
     if (!params || !term_obs || !truncated || !reward || !reward_out || n <= 0)
         return fail(RR_EINVAL, "rr_policy_bootstrap: null argument or n <= 0");
@@ -1692,14 +1717,12 @@ int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int64_t n
     if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_policy_bootstrap: params must be 16-B aligned");
     const dim3 grid((unsigned)((n + pol::kEnvsPerBlock - 1) / pol::kEnvsPerBlock)), block(pol::kThreads);
     hipStream_t s = (hipStream_t)stream;
-    if (obs_dim == 14 && act_dim == 3)
-        hipLaunchKernelGGL((policy_bootstrap_kernel<14, 3>), grid, block, 0, s, params, n, term_obs, truncated,
-                           reward, gamma, reward_out, obs, value_out);
-    else if (obs_dim == 7 && act_dim == 2)
-        hipLaunchKernelGGL((policy_bootstrap_kernel<7, 2>), grid, block, 0, s, params, n, term_obs, truncated, reward,
-                           gamma, reward_out, obs, value_out);
-    else
-        return fail(RR_EINVAL, "rr_policy_bootstrap: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+    const bool ok = pol_dispatch(obs_dim, act_dim, precision, [&](auto c) {
+        using C = decltype(c);
+        hipLaunchKernelGGL((policy_bootstrap_kernel<C::OBS, C::ACT, C::PREC>), grid, block, 0, s, params, n,
+                           term_obs, truncated, reward, gamma, reward_out, obs, value_out);
+    });
+    if (!ok) return RR_POL_UNSUPPORTED("rr_policy_bootstrap");
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_policy_bootstrap: launch");
 }

@@ -60,20 +60,28 @@ class MlpActorCritic(nn.Module):
         return (0.5 + 0.5 * math.log(2 * math.pi) + self.log_std).sum().expand(n)
 
 
-class PolicyPack:
-    """Packs an ``MlpActorCritic``'s weights into the fragment-ordered fp32 buffer of the
-    fused HIP policy kernel (layout: rl_rocket_amd/csrc/rocket_policy.inc, offsets from
-    ``rr_policy_layout``). ``pack()`` is pure device tensor work on the live parameters,
-    so it can sit inside a captured graph and always reflects the current weights."""
+POLICY_PRECISIONS = {"fp32": 0, "bf16": 1}  # RR_POLICY_FP32 / RR_POLICY_BF16
 
-    def __init__(self, policy, obs_dim, act_dim, device):
+
+class PolicyPack:
+    """Packs an ``MlpActorCritic``'s weights into the fragment-ordered buffer of the fused
+    HIP policy kernel (layout: rl_rocket_amd/csrc/rocket_policy.inc, offsets from
+    ``rr_policy_layout``). ``pack()`` is pure device tensor work on the live parameters,
+    so it can sit inside a captured graph and always reflects the current weights.
+    ``precision`` "fp32" (default, SB3-exact to fp32 rounding) or "bf16" (tower weights
+    as bf16 MFMA fragments, opt-in)."""
+
+    def __init__(self, policy, obs_dim, act_dim, device, precision="fp32"):
         import ctypes
 
         from . import _lib
 
+        if precision not in POLICY_PRECISIONS:
+            raise ValueError("precision must be one of %s" % sorted(POLICY_PRECISIONS))
+        self.precision, self.prec = precision, POLICY_PRECISIONS[precision]
         lib = _lib.load()
         off = (ctypes.c_int64 * 12)()
-        size = _lib.check(lib.rr_policy_layout(obs_dim, act_dim, off), "rr_policy_layout")
+        size = _lib.check(lib.rr_policy_layout(obs_dim, act_dim, self.prec, off), "rr_policy_layout")
         self.off = dict(zip(("L1A", "B1", "L2A", "B2", "TOWER", "PI", "VF", "HA", "HV", "HB", "VB", "LS"), list(off)))
         self.size, self.obs_dim, self.act_dim, self.policy = size, obs_dim, act_dim, policy
         self.buf = torch.zeros(size + 4, dtype=torch.float32, device=device)  # +4: 16-B alignment slack
@@ -87,16 +95,34 @@ class PolicyPack:
         def row(rg, h):  # D-layout row of register rg in lane half h
             return (rg & 3) + 8 * (rg >> 2) + 4 * h
 
-        kp1 = (obs_dim + 1) // 2
+        half = torch.arange(2, device=dev)
         m = torch.arange(2, device=dev)
+        # B[m][half][reg] = b[32m + row(reg, half)]
+        self.b_i = (32 * m[:, None, None] + row(reg[None, None, :], half[None, :, None])).reshape(-1)
+        if self.prec:
+            # bf16: L1A[m][s][lane][j] = W1[32m + r][16s + 8hh + j];
+            # L2A[m][t][s][lane][j] = W2[32m + r][32t + 16s + 8(j>>2) + 4hh + (j&3)]
+            kp1 = (obs_dim + 15) // 16
+            s_ = torch.arange(kp1, device=dev)
+            j = torch.arange(8, device=dev)
+            shp1 = (2, kp1, 64, 8)
+            self.l1_i = (32 * m.view(2, 1, 1, 1) + r.view(1, 1, 64, 1)).expand(shp1).reshape(-1)
+            self.l1_k = (16 * s_.view(1, kp1, 1, 1) + 8 * hh.view(1, 1, 64, 1) + j.view(1, 1, 1, 8)).expand(shp1).reshape(-1)
+            t = torch.arange(2, device=dev)
+            shp2 = (2, 2, 2, 64, 8)
+            self.l2_i = (32 * m.view(2, 1, 1, 1, 1) + r.view(1, 1, 1, 64, 1)).expand(shp2).reshape(-1)
+            self.l2_k = (32 * t.view(1, 2, 1, 1, 1) + 16 * torch.arange(2, device=dev).view(1, 1, 2, 1, 1)
+                         + 8 * (j.view(1, 1, 1, 1, 8) >> 2) + 4 * hh.view(1, 1, 1, 64, 1)
+                         + (j.view(1, 1, 1, 1, 8) & 3)).expand(shp2).reshape(-1)
+            self.kp1 = kp1
+            return
+        kp1 = (obs_dim + 1) // 2
+        self.kp1 = kp1
         s_ = torch.arange(kp1, device=dev)
         # L1A[m][s][lane] = W1[32m + r][2s + hh]  (k >= obs_dim -> padded column)
         k1 = 2 * s_[None, :, None] + hh[None, None, :]
         self.l1_i = (32 * m[:, None, None] + r[None, None, :]).expand(2, kp1, 64).reshape(-1)
         self.l1_k = k1.expand(2, kp1, 64).reshape(-1)
-        # B[m][half][reg] = b[32m + row(reg, half)]
-        half = torch.arange(2, device=dev)
-        self.b_i = (32 * m[:, None, None] + row(reg[None, None, :], half[None, :, None])).reshape(-1)
         # L2A[m][t][g][lane][rr] = W2[32m + r][32t + row(4g + rr, hh)]
         t = torch.arange(2, device=dev)
         g = torch.arange(4, device=dev)
@@ -109,11 +135,15 @@ class PolicyPack:
     def _tower(self, net, base):
         o = self.off
         w1, b1, w2, b2 = net[0].weight, net[0].bias, net[2].weight, net[2].bias
-        w1p = torch.nn.functional.pad(w1, (0, 1))  # column obs_dim = 0 (odd obs_dim padding)
-        kp1 = (self.obs_dim + 1) // 2
-        self.buf[base + o["L1A"]: base + o["L1A"] + 2 * kp1 * 64] = w1p[self.l1_i, self.l1_k]
+        kpad = (16 if self.prec else 2) * self.kp1 - self.obs_dim
+        w1p = torch.nn.functional.pad(w1, (0, kpad))  # zero columns past obs_dim
+        l1, l2 = w1p[self.l1_i, self.l1_k], w2[self.l2_i, self.l2_k]
+        if self.prec:  # RNE to bf16; two bf16 per packed float, element 2q in the low half
+            l1 = l1.to(torch.bfloat16).view(torch.float32)
+            l2 = l2.to(torch.bfloat16).view(torch.float32)
+        self.buf[base + o["L1A"]: base + o["L1A"] + l1.numel()] = l1
         self.buf[base + o["B1"]: base + o["B1"] + 64] = b1[self.b_i]
-        self.buf[base + o["L2A"]: base + o["L2A"] + 4096] = w2[self.l2_i, self.l2_k]
+        self.buf[base + o["L2A"]: base + o["L2A"] + l2.numel()] = l2
         self.buf[base + o["B2"]: base + o["B2"] + 64] = b2[self.b_i]
 
     def _sources(self):
@@ -136,8 +166,8 @@ class PolicyPack:
         ts = self._sources()
         src = (ctypes.c_void_p * 13)(*[t.data_ptr() for t in ts])
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.buf.device).cuda_stream)
-        _lib.check(_lib.load().rr_policy_pack(self.obs_dim, self.act_dim, src, ctypes.c_void_p(self.buf.data_ptr()),
-                                              stream), "rr_policy_pack")
+        _lib.check(_lib.load().rr_policy_pack(self.obs_dim, self.act_dim, self.prec, src,
+                                              ctypes.c_void_p(self.buf.data_ptr()), stream), "rr_policy_pack")
         return self.buf
 
     @torch.no_grad()
@@ -161,10 +191,14 @@ class DeviceRollout:
     ``fused=True`` (default for an ``MlpActorCritic`` with 64x64 towers): per step one
     fp32-MFMA HIP launch for policy forward + sampling + buffer writes (``rr_policy_act``),
     the fused env step, one launch for the timeout bootstrap (``rr_policy_bootstrap``);
-    GAE in one launch (``rr_gae``). ``fused=False``: the same algorithm in PyTorch ops."""
+    GAE in one launch (``rr_gae``). ``fused=False``: the same algorithm in PyTorch ops.
+    ``policy_dtype="bf16"`` (fused only, opt-in) runs the towers on bf16 MFMA with fp32
+    accumulation: actions / values / log-probs then differ from the fp32 policy by the bf16
+    rounding of obs, weights and the first hidden layer (the stored log-probs are those of
+    the bf16 mean; PPO's first-epoch ratio starts within ~1e-3 of 1 instead of at 1)."""
 
     def __init__(self, batch, policy, n_steps=16, gamma=0.99, gae_lambda=0.95, generator=None, fused=None,
-                 seed=0):
+                 seed=0, policy_dtype="fp32"):
         self.env, self.policy = batch, policy
         self.n_steps, self.gamma, self.lam = n_steps, gamma, gae_lambda
         n, ns, na = batch.num_envs, batch.state_dim, batch.action_dim
@@ -189,11 +223,16 @@ class DeviceRollout:
         if fused is None:
             fused = isinstance(policy, MlpActorCritic) and policy.hidden == (64, 64) and (ns, na) in ((14, 3), (7, 2))
         self.fused = bool(fused)
+        if policy_dtype not in POLICY_PRECISIONS:
+            raise ValueError("policy_dtype must be one of %s" % sorted(POLICY_PRECISIONS))
+        if policy_dtype != "fp32" and not self.fused:
+            raise ValueError("policy_dtype=%r needs the fused HIP policy path" % policy_dtype)
+        self.policy_dtype = policy_dtype
         if self.fused:
             from . import _lib
 
             self._lib = _lib.load()
-            self._pack = PolicyPack(policy, ns, na, dev)
+            self._pack = PolicyPack(policy, ns, na, dev, precision=policy_dtype)
             self.iter = torch.zeros((1,), dtype=torch.int64, device=dev)  # advanced by every collect (graph-safe)
             self.seed = int(seed) & (2 ** 64 - 1)
             self._ones = torch.ones((n,), dtype=torch.uint8, device=dev)
@@ -246,16 +285,17 @@ class DeviceRollout:
         params = p(self._pack.pack())
         stream = c.c_void_p(torch.cuda.current_stream(env.device).cuda_stream)
         it, obs, done = p(self.iter), p(env.obs), p(env.done)
+        prec = self._pack.prec
         for t in range(self.n_steps):
             prev = t > 0
-            _lib.check(lib.rr_policy_act(params, ns, na, n, env.env_id_offset, obs, self.seed, it, t, p(self._clipped),
+            _lib.check(lib.rr_policy_act(params, ns, na, prec, n, env.env_id_offset, obs, self.seed, it, t, p(self._clipped),
                                          p(self.actions[t]), p(self.values[t]), p(self.log_probs[t]), p(self.obs[t]),
                                          self._term_obs if prev else None, p(env.truncated) if prev else None,
                                          p(env.reward) if prev else None, self.gamma,
                                          p(self.rewards[t - 1]) if prev else None, done, p(self.starts[t]), stream),
                        "rr_policy_act")
             env.step(self._clipped)
-        _lib.check(lib.rr_policy_bootstrap(params, ns, na, n, self._term_obs, p(env.truncated), p(env.reward),
+        _lib.check(lib.rr_policy_bootstrap(params, ns, na, prec, n, self._term_obs, p(env.truncated), p(env.reward),
                                            self.gamma, p(self.rewards[self.n_steps - 1]), obs, p(self.last_value),
                                            stream), "rr_policy_bootstrap")
         self.last_done.copy_(env.done)

@@ -58,7 +58,58 @@ def test_pack_reference_matches_layout(ns, na):
     assert pk.size == o["LS"] + 4
 
 
+@pytest.mark.parametrize("ns,na", [(14, 3), (7, 2)])
+def test_pack_reference_bf16_matches_layout(ns, na):
+    """bf16 tower sections: 8 RNE bf16 per lane and k step, W2 in the permuted k order of
+    an accumulator tile used as the next MFMA's B operand (rocket_policy.inc)."""
+    import torch
+    from rl_rocket_amd.rollout import MlpActorCritic, PolicyPack
+
+    torch.manual_seed(2)
+    pol = MlpActorCritic(ns, na)
+    with torch.no_grad():
+        for p in pol.parameters():
+            p.add_(torch.randn_like(p))
+    pk = PolicyPack(pol, ns, na, torch.device("cpu"), precision="bf16")
+    bits = pk.pack_reference().view(torch.int32).numpy().view(np.uint16)  # 2 bf16 per float, low half first
+    fl = pk.buf.numpy()
+    o = pk.off
+    kp1 = (ns + 15) // 16
+
+    def bf(x):  # RNE bf16 bits of an fp32 value
+        return int(torch.tensor([float(x)], dtype=torch.float32).to(torch.bfloat16).view(torch.int16).item()) & 0xFFFF
+
+    g = lambda t: t.detach().numpy()  # noqa: E731
+    for tw, net in ((o["PI"], pol.pi_net), (o["VF"], pol.vf_net)):
+        w1, b1, w2, b2 = g(net[0].weight), g(net[0].bias), g(net[2].weight), g(net[2].bias)
+        for m in range(2):
+            for s in range(kp1):
+                for lane in range(64):
+                    for j in range(8):
+                        k = 16 * s + 8 * (lane >> 5) + j
+                        ref = bf(w1[32 * m + (lane & 31), k]) if k < ns else 0
+                        assert bits[2 * (tw + o["L1A"]) + ((m * kp1 + s) * 64 + lane) * 8 + j] == ref
+            for half in range(2):
+                for reg in range(16):
+                    assert fl[tw + o["B1"] + (m * 2 + half) * 16 + reg] == b1[32 * m + _row(reg, half)]
+                    assert fl[tw + o["B2"] + (m * 2 + half) * 16 + reg] == b2[32 * m + _row(reg, half)]
+            for t in range(2):
+                for s in range(2):
+                    for lane in range(64):
+                        for j in range(8):
+                            col = 32 * t + 16 * s + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3)
+                            # the same k as D-tile register 8s + j of lane half h
+                            assert col == 32 * t + _row(8 * s + j, lane >> 5)
+                            ref = bf(w2[32 * m + (lane & 31), col])
+                            assert bits[2 * (tw + o["L2A"]) + (((m * 2 + t) * 2 + s) * 64 + lane) * 8 + j] == ref
+    assert o["B1"] == 2 * kp1 * 64 * 4 and o["B2"] - o["L2A"] == 2048
+    assert pk.size == o["LS"] + 4
+
+
 def test_layout_rejects_unsupported_dims():
     from rl_rocket_amd import _lib
 
-    assert _lib.load(require_torch=False).rr_policy_layout(10, 3, None) == _lib.RR_EINVAL
+    lib = _lib.load(require_torch=False)
+    assert lib.rr_policy_layout(10, 3, _lib.RR_POLICY_FP32, None) == _lib.RR_EINVAL
+    assert lib.rr_policy_layout(14, 3, 2, None) == _lib.RR_EINVAL  # unknown precision
+    assert lib.rr_policy_layout(14, 3, _lib.RR_POLICY_BF16, None) < lib.rr_policy_layout(14, 3, 0, None)
