@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--policy-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="rollout mode: fused policy towers on fp32 MFMA (SB3-exact, default) or bf16 MFMA "
                          "with fp32 accumulation (opt-in)")
+    ap.add_argument("--rollout-two-launch", action="store_true",
+                    help="rollout mode: rr_policy_act + rr_step per step instead of the one-launch rr_rollout_step")
     ap.add_argument("--rollout-torch", action="store_true",
                     help="rollout policy / bootstrap / GAE as PyTorch ops instead of the fused HIP kernels")
     return ap.parse_args()
@@ -67,8 +69,9 @@ def bench_rollout(args, dev, n, model, kw):
     env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
                       episode_stats=False, integrator=args.integrator, **kw)
     pol = MlpActorCritic(env.state_dim, env.action_dim).to(dev)
-    ro = DeviceRollout(env, pol, n_steps=args.rollout_steps, fused=not args.rollout_torch,
-                       policy_dtype=args.policy_dtype)
+    fused = not args.rollout_torch
+    ro = DeviceRollout(env, pol, n_steps=args.rollout_steps, fused=fused, policy_dtype=args.policy_dtype,
+                       one_launch=fused and not args.rollout_two_launch and args.integrator != "dopri5")
     for _ in range(3):
         ro.collect()
     torch.cuda.synchronize(dev)
@@ -109,7 +112,8 @@ def bench_rollout(args, dev, n, model, kw):
                                "+ timeout bootstrap + rollout buffer + GAE, n_steps=%d per hipGraph"
                                % (n, args.rollout_steps), "envs_per_gpu": n,
                    "policy_path": "PyTorch ops" if args.rollout_torch else
-                   "fused HIP (%s MFMA) rr_policy_act" % args.policy_dtype},
+                   ("one launch per step: rr_rollout_step (policy on %s MFMA + env step)" if ro.one_launch else
+                    "two launches per step: rr_policy_act (%s MFMA) + rr_step") % args.policy_dtype},
         "gpu_ms_per_collect": e0.elapsed_time(e1) / reps,
         "ppo_epoch_ms": upd * 1e3, "ppo_stats": stats,
     }

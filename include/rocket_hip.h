@@ -219,10 +219,26 @@ int rr_policy_act(const float* params, int obs_dim, int act_dim, int precision, 
                   const uint8_t* done, float* start_out, void* stream);
 
 /* End of a rollout: reward_out[i] = reward[i] + gamma * V(term_obs[i]) where truncated[i]
- * (TimeLimit.truncated), else reward[i]; and, if value_out != NULL, value_out[i] = V(obs[i]). */
+ * (TimeLimit.truncated), else reward[i] (skipped when term_obs == NULL); and, if
+ * value_out != NULL, value_out[i] = V(obs[i]). */
 int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int precision, int64_t n,
                         const float* term_obs, const uint8_t* truncated, const float* reward, float gamma,
                         float* reward_out, const float* obs, float* value_out, void* stream);
+
+/* One rollout step in ONE launch: rr_policy_act (without its previous-step bookkeeping) and
+ * rr_step fused. For every env i of e: obs = state * normalizer^-1 (the obs rr_step /
+ * rr_reset last produced) -> buf_obs [n][obs_dim]; a ~ N(mean, exp(log_std)) with the noise
+ * key of rr_policy_act (seed, env id, *iter, t) -> buf_action [n][act_dim] (unclipped),
+ * buf_value, buf_log_prob; the env steps with clip(a, -1, 1) (auto-reset, TimeLimit, terminal
+ * rows as rr_step); buf_reward[i] = reward + gamma * V(terminal obs) where truncated;
+ * buf_start[i] = done[i] as passed in (the previous step's done flags, updated in place to
+ * this step's). reward / done (required), truncated / terms (optional) are rr_step's env
+ * outputs; obs (optional, NULL to skip) receives the post-step obs. Bitwise the same results
+ * as rr_policy_act + rr_step. RK4 / Euler envs (not RR_INT_DOPRI5). */
+int rr_rollout_step(rr_env* e, const float* params, int precision, uint64_t seed, const uint64_t* iter, int t,
+                    float gamma, float* buf_obs, float* buf_action, float* buf_value, float* buf_log_prob,
+                    float* buf_start, float* buf_reward, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
+                    float* terms, void* stream);
 
 /* RolloutBuffer.compute_returns_and_advantage: rewards / values / starts [T][n] (starts[t]
  * = episode-start flag of step t), last_value / last_done [n] -> advantages, returns [T][n]. */

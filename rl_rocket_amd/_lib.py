@@ -106,6 +106,8 @@ SIGNATURES = {
                                      ctypes.c_float, _P, _P, _P, _P]),
     "rr_policy_bootstrap": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _P, _P, _P,
                                            ctypes.c_float, _P, _P, _P, _P]),
+    "rr_rollout_step": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_uint64, _P, ctypes.c_int, ctypes.c_float,
+                                       _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rr_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, _P,
                               _P, _P]),
 }

@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "rocket_hip.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc")]
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc", "rocket_rollout.inc")]
 HEADER = os.path.join(ROOT, "include", "rocket_hip.h")
 OUT = os.path.join(HERE, "librocket_hip.so")
 ARCH = os.environ.get("RR_OFFLOAD_ARCH", "gfx950")
@@ -23,13 +23,19 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def command(resource_usage=False, out=OUT, defines=()):
+def command(resource_usage=False, out=OUT, defines=(), extra=()):
     # -fno-slp-vectorize: the SLP pass packs scalar f32 math into v_pk_* pairs and adds ~180
     # register moves to the step kernel (measured on the .s); the scalar stream is shorter.
+    # -ffp-contract=on: a*b+c becomes an fma only inside one source expression. HIP's default
+    # (fast) also fuses across statements in the backend, and what it fuses depends on the
+    # basic-block layout around inlined code: the env step inlined into rr_rollout_step then
+    # rounded differently from step_kernel (1 ulp in 0.2 % of envs). Expression-level
+    # contraction makes every kernel that inlines the physics compute the same bits.
     # kernarg preload: the step kernel's leading pointer / word arguments arrive in user SGPRs
-    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-fno-slp-vectorize", "-std=c++17", "-fPIC", "-shared",
-           "-mllvm", "-amdgpu-kernarg-preload-count=4",
-           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")] + ["-D%s" % d for d in defines] + ["-o", out, SRC]
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-fno-slp-vectorize", "-ffp-contract=on", "-std=c++17",
+           "-fPIC", "-shared", "-mllvm", "-amdgpu-kernarg-preload-count=4",
+           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")] + list(extra) + \
+        ["-D%s" % d for d in defines] + ["-o", out, SRC]
     if resource_usage:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     return cmd

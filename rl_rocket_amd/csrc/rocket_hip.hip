@@ -1070,6 +1070,7 @@ __global__ __launch_bounds__(kBlock) void gather_done_kernel(const int32_t* idx,
 
 // On-device PPO rollout kernels (fused MlpPolicy forward on fp32 MFMA, bootstrap, GAE)
 #include "rocket_policy.inc"
+#include "rocket_rollout.inc"
 
 // Exact-integrator mode (RR_INT_DOPRI5): fp64 scipy RK45 restatement, compiled without
 // FMA contraction so its roundings follow the reference's numpy arithmetic.
@@ -1711,8 +1712,10 @@ int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int preci
                         const float* term_obs, const uint8_t* truncated, const float* reward, float gamma,
                         float* reward_out, const float* obs, float* value_out, void* stream)
 {
-    if (!params || !term_obs || !truncated || !reward || !reward_out || n <= 0)
-        return fail(RR_EINVAL, "rr_policy_bootstrap: null argument or n <= 0");
+    if (!params || n <= 0) return fail(RR_EINVAL, "rr_policy_bootstrap: null params or n <= 0");
+    if (term_obs && (!truncated || !reward || !reward_out))
+        return fail(RR_EINVAL, "rr_policy_bootstrap: term_obs needs truncated, reward, reward_out");
+    if (!term_obs && !value_out) return fail(RR_EINVAL, "rr_policy_bootstrap: nothing to do");
     if (value_out && !obs) return fail(RR_EINVAL, "rr_policy_bootstrap: value_out needs obs");
     if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_policy_bootstrap: params must be 16-B aligned");
     const dim3 grid((unsigned)((n + pol::kEnvsPerBlock - 1) / pol::kEnvsPerBlock)), block(pol::kThreads);
@@ -1725,6 +1728,70 @@ int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int preci
     if (!ok) return RR_POL_UNSUPPORTED("rr_policy_bootstrap");
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_policy_bootstrap: launch");
+}
+
+int rr_rollout_step(rr_env* e, const float* params, int precision, uint64_t seed, const uint64_t* iter, int t,
+                    float gamma, float* buf_obs, float* buf_action, float* buf_value, float* buf_log_prob,
+                    float* buf_start, float* buf_reward, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
+                    float* terms, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_rollout_step: null handle");
+    if (!params || !iter || !buf_obs || !buf_action || !buf_value || !buf_log_prob || !buf_start || !buf_reward ||
+        !reward || !done)
+        return fail(RR_EINVAL, "rr_rollout_step: null argument");
+    if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_rollout_step: params must be 16-B aligned");
+    if (precision != RR_POLICY_FP32 && precision != RR_POLICY_BF16)
+        return fail(RR_EINVAL, "rr_rollout_step: precision must be RR_POLICY_FP32 or RR_POLICY_BF16");
+    if (e->p.integrator == RR_INT_DOPRI5)
+        return fail(RR_EINVAL, "rr_rollout_step: RR_INT_DOPRI5 envs step through rr_policy_act + rr_step");
+    RolloutIO io;
+    io.params = params;
+    io.iter = iter;
+    io.buf_obs = buf_obs;
+    io.buf_act = buf_action;
+    io.buf_val = buf_value;
+    io.buf_logp = buf_log_prob;
+    io.buf_start = buf_start;
+    io.buf_rew = buf_reward;
+    io.obs = obs;
+    io.reward = reward;
+    io.done = done;
+    io.truncated = truncated;
+    io.terms = terms;
+    io.seed_lo = (uint32_t)seed;
+    io.seed_hi = (uint32_t)(seed >> 32);
+    io.t = (uint32_t)t;
+    io.gamma = gamma;
+    io.obs_vec_ok = ((uintptr_t)obs & 15u) == 0;
+    io.buf_obs_vec_ok = ((uintptr_t)buf_obs & 15u) == 0;
+    const Bufs b = bufs_of(e);
+    const uint32_t nn = (uint32_t)e->n;
+    const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
+    const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
+    const dim3 grid((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock)), block(rol::kThreads);
+    hipStream_t s = (hipStream_t)stream;
+    const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
+    const bool bf = precision == RR_POLICY_BF16;
+#define RR_LAUNCH(M, I, PR) \
+    hipLaunchKernelGGL((rollout_step_kernel<M, I, PR>), grid, block, 0, s, e->state, nn, mode, e->kp, b, io)
+    if (m6 && !euler) {
+        if (bf) RR_LAUNCH(6, RR_INT_RK4, 1);
+        else RR_LAUNCH(6, RR_INT_RK4, 0);
+    } else if (m6) {
+        if (bf) RR_LAUNCH(6, RR_INT_EULER, 1);
+        else RR_LAUNCH(6, RR_INT_EULER, 0);
+    } else if (!euler) {
+        if (bf) RR_LAUNCH(3, RR_INT_RK4, 1);
+        else RR_LAUNCH(3, RR_INT_RK4, 0);
+    } else {
+        if (bf) RR_LAUNCH(3, RR_INT_EULER, 1);
+        else RR_LAUNCH(3, RR_INT_EULER, 0);
+    }
+#undef RR_LAUNCH
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return hip_fail(err, "rr_rollout_step: launch");
+    e->steps++;
+    return RR_OK;
 }
 
 int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, const float* starts,

@@ -192,13 +192,16 @@ class DeviceRollout:
     fp32-MFMA HIP launch for policy forward + sampling + buffer writes (``rr_policy_act``),
     the fused env step, one launch for the timeout bootstrap (``rr_policy_bootstrap``);
     GAE in one launch (``rr_gae``). ``fused=False``: the same algorithm in PyTorch ops.
+    ``one_launch=True`` (default where possible: fused, RK4 / Euler env) collapses each step
+    to ONE launch (``rr_rollout_step``: policy, sample, env step, bootstrap and buffer writes
+    in one kernel); bitwise the same rollout as the two-launch sequence.
     ``policy_dtype="bf16"`` (fused only, opt-in) runs the towers on bf16 MFMA with fp32
     accumulation: actions / values / log-probs then differ from the fp32 policy by the bf16
     rounding of obs, weights and the first hidden layer (the stored log-probs are those of
     the bf16 mean; PPO's first-epoch ratio starts within ~1e-3 of 1 instead of at 1)."""
 
     def __init__(self, batch, policy, n_steps=16, gamma=0.99, gae_lambda=0.95, generator=None, fused=None,
-                 seed=0, policy_dtype="fp32"):
+                 seed=0, policy_dtype="fp32", one_launch=None):
         self.env, self.policy = batch, policy
         self.n_steps, self.gamma, self.lam = n_steps, gamma, gae_lambda
         n, ns, na = batch.num_envs, batch.state_dim, batch.action_dim
@@ -228,6 +231,12 @@ class DeviceRollout:
         if policy_dtype != "fp32" and not self.fused:
             raise ValueError("policy_dtype=%r needs the fused HIP policy path" % policy_dtype)
         self.policy_dtype = policy_dtype
+        dopri = self.fused and int(batch.params.integrator) == 2  # RR_INT_DOPRI5: two-launch path
+        if one_launch is None:
+            one_launch = self.fused and not dopri
+        if one_launch and (not self.fused or dopri):
+            raise ValueError("one_launch needs the fused policy and an RK4 / Euler env")
+        self.one_launch = bool(one_launch)
         if self.fused:
             from . import _lib
 
@@ -275,9 +284,10 @@ class DeviceRollout:
         self._gae()
 
     def _collect_fused(self):
-        """Two launches per step: rr_policy_act (forward + sample of step t, bootstrap of
-        step t-1, episode-start flags) and the fused env step; obs are read in place from
-        the env's output buffer."""
+        """one_launch: one rr_rollout_step per step (the env's obs buffer is written on the
+        last step only), then V(last obs). Otherwise two launches per step: rr_policy_act
+        (forward + sample of step t, bootstrap of step t-1, episode-start flags) and the
+        fused env step; obs are read in place from the env's output buffer."""
         env, lib, c, p = self.env, self._lib, self._c, self._p
         from . import _lib
 
@@ -286,6 +296,18 @@ class DeviceRollout:
         stream = c.c_void_p(torch.cuda.current_stream(env.device).cuda_stream)
         it, obs, done = p(self.iter), p(env.obs), p(env.done)
         prec = self._pack.prec
+        if self.one_launch:
+            T = self.n_steps
+            for t in range(T):
+                _lib.check(lib.rr_rollout_step(env._h, params, prec, self.seed, it, t, self.gamma, p(self.obs[t]),
+                                               p(self.actions[t]), p(self.values[t]), p(self.log_probs[t]),
+                                               p(self.starts[t]), p(self.rewards[t]), obs if t == T - 1 else None,
+                                               p(env.reward), done, p(env.truncated), p(env.terms), stream),
+                           "rr_rollout_step")
+            _lib.check(lib.rr_policy_bootstrap(params, ns, na, prec, n, None, None, None, self.gamma, None, obs,
+                                               p(self.last_value), stream), "rr_policy_bootstrap")
+            self._finish(stream)
+            return
         for t in range(self.n_steps):
             prev = t > 0
             _lib.check(lib.rr_policy_act(params, ns, na, prec, n, env.env_id_offset, obs, self.seed, it, t, p(self._clipped),
@@ -298,6 +320,15 @@ class DeviceRollout:
         _lib.check(lib.rr_policy_bootstrap(params, ns, na, prec, n, self._term_obs, p(env.truncated), p(env.reward),
                                            self.gamma, p(self.rewards[self.n_steps - 1]), obs, p(self.last_value),
                                            stream), "rr_policy_bootstrap")
+        self._finish(stream)
+
+    def _finish(self, stream):
+        """last_done / last_start from the env's done flags, GAE (rr_gae), advance the
+        noise counter."""
+        from . import _lib
+
+        env, lib, p = self.env, self._lib, self._p
+        n = env.num_envs
         self.last_done.copy_(env.done)
         self.last_start.copy_(env.done)
         _lib.check(lib.rr_gae(self.n_steps, n, p(self.rewards), p(self.values), p(self.starts), p(self.last_value),

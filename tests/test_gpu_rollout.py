@@ -241,3 +241,44 @@ def test_fused_collect_matches_semantics(fused, prec):
     torch.cuda.synchronize()
     assert torch.isfinite(ro.rewards).all() and not torch.equal(a0, ro.actions)
     env.close()
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("model", [6, 3])
+def test_one_launch_rollout_bitwise_equals_two_launch(model, prec):
+    """rr_rollout_step (policy + env step in one kernel) against rr_policy_act + rr_step:
+    every rollout buffer, the env outputs and the env state bitwise equal over two collects
+    (TimeLimit 6 < n_steps: truncation bootstraps and auto-resets inside the rollout; ragged
+    N: idle waves in the last workgroup)."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout
+
+    n, T = 4096 + 37, 8
+    ns, na = (14, 3) if model == 6 else (7, 2)
+    kw = ENV_CONFIG_6DOF if model == 6 else {}
+    pol = _policy(ns, na, seed=3)
+    ros = []
+    for one in (False, True):
+        env = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=6, **kw)
+        ro = DeviceRollout(env, pol, n_steps=T, policy_dtype=prec, one_launch=one, seed=11)
+        assert ro.one_launch == one
+        ros.append(ro)
+    for _ in range(2):
+        for ro in ros:
+            ro.collect()
+        torch.cuda.synchronize()
+        a, b = ros
+        for name in ("obs", "actions", "values", "log_probs", "starts", "rewards", "advantages", "returns",
+                     "last_value", "last_done"):
+            x, y = getattr(a, name), getattr(b, name)
+            assert torch.equal(x, y), (name, (x - y).abs().max().item())
+        for name in ("obs", "reward", "done", "truncated"):
+            assert torch.equal(getattr(a.env, name), getattr(b.env, name)), name
+        sa, sb = a.env.get_state(), b.env.get_state()
+        for x, y in zip(sa, sb):
+            assert torch.equal(x, y)
+    assert a.starts[1:].sum() > 0 and (a.rewards != 0).any()
+    for ro in ros:
+        ro.env.close()

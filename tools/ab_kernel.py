@@ -1,6 +1,7 @@
 """Interleaved A/B timing of kernel source variants on ONE GPU.
 
     python tools/ab_kernel.py A.hip B.hip [...] [--n 65536] [--rounds 5] [--model 6]
+    (a source may carry "@NAME=VAL,+-compiler-flag,..." defines / extra flags)
 
 Each variant is compiled with the product flags (rl_rocket_amd/build.py) into its own
 .so; rounds alternate A, B, A, B ... each in a fresh child process (tools/diag_kernel.py
@@ -34,7 +35,9 @@ def main():
     for k, spec in enumerate(a.sources):
         src, _, defs = spec.partition("@")  # "file.hip@NAME=VAL,NAME2=VAL2"
         lib = os.path.join(a.out, "ab_%d.so" % k)
-        cmd = b.command(out=lib, defines=tuple(d for d in defs.split(",") if d))
+        items = [d for d in defs.split(",") if d]  # "+flag" items are extra compiler flags
+        cmd = b.command(out=lib, defines=tuple(d for d in items if not d.startswith("+")),
+                        extra=tuple(d[1:] for d in items if d.startswith("+")))
         cmd[-1] = os.path.abspath(src)
         subprocess.check_call(cmd)
         libs.append(lib)
