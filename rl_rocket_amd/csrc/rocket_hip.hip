@@ -46,6 +46,12 @@ namespace {
 #ifndef RR_RK4_GENERIC  // 1 = generic 14-component RK4 for 6DOF too (A/B reference)
 #define RR_RK4_GENERIC 0
 #endif
+#ifndef RR_RK4_PACKED  // 1 = 6DOF RK4 on packed fp32 pairs (v_pk_fma_f32)
+#define RR_RK4_PACKED 1
+#endif
+#ifndef RR_OBS_PACKED
+#define RR_OBS_PACKED 1
+#endif
 #ifndef RR_EARLY_RESET  // 1 = draw the auto-reset candidate during the load wait
 #define RR_EARLY_RESET 1
 #endif
@@ -63,6 +69,18 @@ namespace {
 // in the end-of-kernel writeback (A/B at N = 65536: 5.49 -> 5.18 us; the same bit on the
 // state planes, which the next launch re-reads, is slower; nt loads +5 %).
 #define RR_OUT_AUX 16
+#endif
+#ifndef RR_STAGGER  // experiment: number of start-delay groups (0 = off)
+#define RR_STAGGER 0
+#endif
+#ifndef RR_STAGGER_BY
+#define RR_STAGGER_BY 0
+#endif
+#ifndef RR_STAGGER_SLEEP
+#define RR_STAGGER_SLEEP 8
+#endif
+#ifndef RR_STEP_ATTR  // occupancy floor of the step kernel: <= 128 VGPRs keeps 4 waves per SIMD at large N
+#define RR_STEP_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
 #ifndef RR_BLOCK
 #define RR_BLOCK 256
@@ -193,7 +211,7 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
 
 struct Bufs {
 #if RR_DIAG == 4
-    uint64_t* stamps;         // [waves][10]: 8 s_memtime phase stamps, s_memrealtime at start / end
+    uint64_t* stamps;         // [waves][12]: 8 s_memtime phase stamps, s_memrealtime at start / end, XCC_ID, HW_ID
 #endif
     float* state;
     float* v0;
@@ -217,6 +235,15 @@ struct StepIO {
 };
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// packed fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 with op_sel swizzles)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_swap(f2 a) { return __builtin_shufflevector(a, a, 1, 0); }
+__device__ __forceinline__ f2 pk_lo(f2 a) { return __builtin_shufflevector(a, a, 0, 0); }
+__device__ __forceinline__ f2 pk_hi(f2 a) { return __builtin_shufflevector(a, a, 1, 1); }
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 pk_his(f2 a, f2 b) { return __builtin_shufflevector(a, b, 1, 3); }  // (a.hi, b.hi)
+__device__ __forceinline__ f2 pk_bc(float x) { return f2{x, x}; }
 
 #if RR_DIAG == 4
 #define RR_STAMP(k)                                                                     \
@@ -530,6 +557,142 @@ __device__ __forceinline__ void integrate6_rk4(const KParams& P, const Ctl& c, c
     f0[13] = c.dm;
 }
 
+// The same specialised RK4 on packed fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32, two lanes'
+// worth of fp32 per instruction): a lone wave issues one VALU instruction per 4 cycles
+// whatever its width, so pairing the independent components of one env halves the issue
+// cost of the quaternion and angular-rate algebra. Pairs: q = (q0,q1),(q2,q3);
+// W = (W2,W3); a = (ax,ay), az. Each half rounds exactly like the scalar fma.
+
+// o = y * inv_norm, two components per v_pk_mul_f32
+template <int NS>
+__device__ __forceinline__ void normalize_obs(const float* y, const float* inv_norm, float* o)
+{
+#if RR_OBS_PACKED
+#pragma unroll
+    for (int j = 0; j + 1 < NS; j += 2) {
+        const f2 v = f2{y[j], y[j + 1]} * f2{inv_norm[j], inv_norm[j + 1]};
+        o[j] = v.x;
+        o[j + 1] = v.y;
+    }
+    if constexpr (NS % 2) o[NS - 1] = y[NS - 1] * inv_norm[NS - 1];
+#else
+#pragma unroll
+    for (int j = 0; j < NS; ++j) o[j] = y[j] * inv_norm[j];
+#endif
+}
+
+__device__ __forceinline__ void integrate6_rk4_pk(const KParams& P, const Ctl& c, const float* y0, float* y1,
+                                                  float* f0)
+{
+    const float h = P.h, hh = P.h2, h6 = P.h6, hh6 = P.h * P.h6;
+    const f2 t2xy = {2.0f * c.tbx, 2.0f * c.tby};
+    const float t2z = 2.0f * c.tbz;
+    const f2 tbxy = {c.tbx, c.tby};
+    const f2 t2zn = {t2z, -t2z}, t2yx = {-t2xy.y, t2xy.x};
+    const f2 gxy = {-kG0, 0.0f};
+    // R(q) T_b / m + g with the unnormalised q (see rhs): pair (ax, ay) and az
+    auto accel = [&](f2 q01, f2 q23, float m, f2& axy, float& az) {
+        const f2 sq = pk_fma(q01, q01, q23 * q23);
+        const float qq = sq.x + sq.y;
+        // t = 2 u x T_b, u = (q1, q2, q3), with qa = (q2, q1):
+        //   (tx, ty) = qa (t2z, -t2z) + q3 (-t2y, t2x),   tz = q1 t2y - q2 t2x
+        const f2 qa = __builtin_shufflevector(q23, q01, 0, 3);
+        const f2 q3 = pk_hi(q23);
+        const f2 txy = pk_fma(qa, t2zn, q3 * t2yx);
+        const float tz = fmaf(q01.y, t2xy.y, -q23.x * t2xy.x);
+        // F = |q|^2 T_b + q0 t + u x t;  (u x t)_xy = qa (tz, -tz) + q3 (-ty, tx)
+        const f2 uxt = pk_fma(qa, f2{tz, -tz}, q3 * (pk_swap(txy) * f2{-1.0f, 1.0f}));
+        const f2 Fxy = pk_fma(pk_bc(qq), tbxy, pk_fma(pk_lo(q01), txy, uxt));
+        const float Fz = fmaf(qq, c.tbz, fmaf(q01.x, tz, fmaf(q01.y, txy.y, -q23.x * txy.x)));
+        const float sc = frcp(qq * m);
+        axy = pk_fma(Fxy, pk_bc(sc), gxy);
+        az = Fz * sc;
+    };
+    const float W1 = 0.5f * y0[10];
+    // dW2 = A2 + B2 W3, dW3 = A3 + B3 W2 (half of dw = J^-1 (tau - w x Jw)): pair form
+    // dW = A + B swap(W)
+    const f2 A = {0.5f * c.tau1, 0.5f * c.tau2};
+    const f2 B = {(-2.0f * kJd1 * kJinv2) * W1, (-2.0f * kJd2 * kJinv3) * W1};
+    // dq = Omega(W) q:
+    //   (d0, d1) = (-W1, W1) (q1, q0) + (-W2, W3) (q2, q2) - (W3, W2) (q3, q3)
+    //   (d2, d3) = (W2, W3) (q0, q0) + (-W3, W2) (q1, q1) + (W1, -W1) (q3, q2)
+    const f2 w1a = {-W1, W1}, w1b = {W1, -W1};
+    auto dq = [&](f2 q01, f2 q23, f2 W, f2& d01, f2& d23) {
+        const f2 Wn = W * f2{-1.0f, 1.0f}, Ws = pk_swap(W), Wsn = Ws * f2{-1.0f, 1.0f};
+        d01 = pk_fma(w1a, pk_swap(q01), pk_fma(Wn, pk_lo(q23), -(Ws * pk_hi(q23))));
+        d23 = pk_fma(W, pk_lo(q01), pk_fma(Wsn, pk_hi(q01), w1b * pk_swap(q23)));
+    };
+    const f2 q01 = {y0[6], y0[7]}, q23 = {y0[8], y0[9]};
+    const f2 W0 = {0.5f * y0[11], 0.5f * y0[12]};
+    const float m0 = y0[13];
+    const float mh = m0 + hh * c.dm, me = m0 + h * c.dm;
+    const f2 hh2 = pk_bc(hh), h2 = pk_bc(h);
+    f2 a1, a2, a3, a4, k101, k123, k201, k223, k301, k323, k401, k423, l1, l2, l3, l4;
+    float a1z, a2z, a3z, a4z;
+    // stage 1
+    accel(q01, q23, m0, a1, a1z);
+    dq(q01, q23, W0, k101, k123);
+    l1 = pk_fma(B, pk_swap(W0), A);
+    // stage 2
+    f2 Ws = pk_fma(hh2, l1, W0);
+    f2 qs01 = pk_fma(hh2, k101, q01), qs23 = pk_fma(hh2, k123, q23);
+    accel(qs01, qs23, mh, a2, a2z);
+    dq(qs01, qs23, Ws, k201, k223);
+    l2 = pk_fma(B, pk_swap(Ws), A);
+    // stage 3
+    Ws = pk_fma(hh2, l2, W0);
+    qs01 = pk_fma(hh2, k201, q01);
+    qs23 = pk_fma(hh2, k223, q23);
+    accel(qs01, qs23, mh, a3, a3z);
+    dq(qs01, qs23, Ws, k301, k323);
+    l3 = pk_fma(B, pk_swap(Ws), A);
+    // stage 4
+    Ws = pk_fma(h2, l3, W0);
+    qs01 = pk_fma(h2, k301, q01);
+    qs23 = pk_fma(h2, k323, q23);
+    accel(qs01, qs23, me, a4, a4z);
+    dq(qs01, qs23, Ws, k401, k423);
+    l4 = pk_fma(B, pk_swap(Ws), A);
+    // updates: v1 = v0 + h/6 (a1 + 2 a2 + 2 a3 + a4), r1 = r0 + h v0 + h^2/6 (a1 + a2 + a3)
+    const f2 two = pk_bc(2.0f), h62 = pk_bc(h6), hh62 = pk_bc(hh6);
+    const f2 v01 = {y0[3], y0[4]}, r01 = {y0[0], y0[1]};
+    const f2 s23 = a2 + a3;
+    const f2 v1 = pk_fma(h62, pk_fma(two, s23, a1 + a4), v01);
+    const f2 r1 = pk_fma(hh62, a1 + s23, pk_fma(h2, v01, r01));
+    const float s23z = a2z + a3z;
+    y1[0] = r1.x;
+    y1[1] = r1.y;
+    y1[2] = (y0[2] + h * y0[5]) + hh6 * (a1z + s23z);
+    y1[3] = v1.x;
+    y1[4] = v1.y;
+    y1[5] = y0[5] + h6 * (a1z + a4z + 2.0f * s23z);
+    const f2 qe01 = pk_fma(h62, pk_fma(two, k201 + k301, k101 + k401), q01);
+    const f2 qe23 = pk_fma(h62, pk_fma(two, k223 + k323, k123 + k423), q23);
+    const f2 We = pk_fma(h62, pk_fma(two, l2 + l3, l1 + l4), W0);
+    y1[6] = qe01.x;
+    y1[7] = qe01.y;
+    y1[8] = qe23.x;
+    y1[9] = qe23.y;
+    y1[10] = y0[10];
+    y1[11] = 2.0f * We.x;
+    y1[12] = 2.0f * We.y;
+    y1[13] = me;
+    f0[0] = y0[3];
+    f0[1] = y0[4];
+    f0[2] = y0[5];
+    f0[3] = a1.x;
+    f0[4] = a1.y;
+    f0[5] = a1z;
+    f0[6] = k101.x;
+    f0[7] = k101.y;
+    f0[8] = k123.x;
+    f0[9] = k123.y;
+    f0[10] = 0.0f;
+    f0[11] = 2.0f * l1.x;
+    f0[12] = 2.0f * l1.y;
+    f0[13] = c.dm;
+}
+
 template <int MODEL, int INTEG>
 __device__ __forceinline__ void integrate(const KParams& P, const Ctl& c, const float* y0, float h,
                                           float* y1, float* f0)
@@ -538,7 +701,11 @@ __device__ __forceinline__ void integrate(const KParams& P, const Ctl& c, const 
     float k[NS], yt[NS];
 #if !RR_RK4_GENERIC
     if constexpr (MODEL == 6 && INTEG == RR_INT_RK4) {
+#if RR_RK4_PACKED
+        integrate6_rk4_pk(P, c, y0, y1, f0);
+#else
         integrate6_rk4(P, c, y0, y1, f0);
+#endif
         return;
     }
 #endif
@@ -597,6 +764,11 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
     rhs<MODEL>(P, c, y1, f1);
     if (x0 != 0.0f) {
         const float hv0 = P.h * f0[EV], hv1 = P.h * f1[EV];
+        // the altitude's Hermite cubic in monomial form: H(s) = ((c3 s + c2) s + c1) s + c0
+        const float dx = x1 - x0;
+        const float c2 = 3.0f * dx - (2.0f * hv0 + hv1), c3 = (hv0 + hv1) - 2.0f * dx;
+        const float d2 = 2.0f * c2, d3 = 3.0f * c3;
+        const bool pos0 = x0 > 0.0f;
         float lo = 0.0f, hi = 1.0f;  // H(lo) has the sign of x0
         s = x0 * frcp(x0 - x1);
         // Newton from the secant guess, kept inside the closed sign bracket [lo, hi]
@@ -605,23 +777,59 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         // guess; the parity tests cover touchdowns down to |v| ~ 1 m/s).
 #pragma unroll
         for (int it = 0; it < RR_NEWTON_ITERS; ++it) {
-            const float s2 = s * s, s3 = s2 * s;
-            const float H = (2 * s3 - 3 * s2 + 1) * x0 + (s3 - 2 * s2 + s) * hv0 + (3 * s2 - 2 * s3) * x1 +
-                            (s3 - s2) * hv1;
-            const float dH = (6 * s2 - 6 * s) * (x0 - x1) + (3 * s2 - 4 * s + 1) * hv0 + (3 * s2 - 2 * s) * hv1;
-            const bool same = (H > 0.0f) == (x0 > 0.0f);
+            const float H = fmaf(fmaf(fmaf(c3, s, c2), s, hv0), s, x0);
+            const float dH = fmaf(fmaf(d3, s, d2), s, hv0);
+            const bool same = (H > 0.0f) == pos0;
             lo = same ? s : lo;
             hi = same ? hi : s;
-            float sn = s - H * frcp(dH);
+            float sn = fmaf(-H, frcp(dH), s);
             sn = (sn >= lo && sn <= hi) ? sn : 0.5f * (lo + hi);
             s = (H == 0.0f) ? s : sn;
         }
     }
+    // every component at the root: y = y0 + h01 (y1 - y0) + h10 f0 + h11 f1 (cubic Hermite)
     const float s2 = s * s, s3 = s2 * s;
-    const float h00 = 2 * s3 - 3 * s2 + 1, h01 = 3 * s2 - 2 * s3;
+    const float h01 = 3 * s2 - 2 * s3;
     const float h10 = P.h * (s3 - 2 * s2 + s), h11 = P.h * (s3 - s2);
-#pragma unroll
-    for (int j = 0; j < NS; ++j) y1[j] = h00 * y0[j] + h01 * y1[j] + h10 * f0[j] + h11 * f1[j];
+    // two components per v_pk_fma_f32; w1 (6DOF) is constant over the step (J2 == J3) and the
+    // mass is linear in t, so exact at the root
+    const f2 H01 = {h01, h01}, H10 = {h10, h10}, H11 = {h11, h11};
+    auto herm2 = [&](int j, int k) {
+        const f2 a = {y0[j], y0[k]}, b = {y1[j], y1[k]};
+        const f2 r = pk_fma(H11, f2{f1[j], f1[k]}, pk_fma(H10, f2{f0[j], f0[k]}, pk_fma(H01, b - a, a)));
+        y1[j] = r.x;
+        y1[k] = r.y;
+    };
+    herm2(0, 1);
+    herm2(2, 3);
+    herm2(4, 5);
+    if constexpr (MODEL == 6) {
+        herm2(6, 7);
+        herm2(8, 9);
+        herm2(11, 12);
+    }
+    y1[NS - 1] = fmaf(s * P.h, f0[NS - 1], y0[NS - 1]);
+}
+
+// After the step: _normalize_quaternion (simulator.py:250) / _wrapTo2Pi (simulator.py:150-163)
+template <int MODEL>
+__device__ __forceinline__ void post_integrate(float* y1)
+{
+    if constexpr (MODEL == 6) {
+        // _normalize_quaternion (simulator.py:250)
+        const f2 q01 = {y1[6], y1[7]}, q23 = {y1[8], y1[9]};
+        const f2 sq = pk_fma(q01, q01, q23 * q23);
+        const f2 rn = pk_bc(frsq(sq.x + sq.y));
+        const f2 n01 = q01 * rn, n23 = q23 * rn;
+        y1[6] = n01.x;
+        y1[7] = n01.y;
+        y1[8] = n23.x;
+        y1[9] = n23.y;
+    } else {
+        // _wrapTo2Pi (simulator.py:150-163): fmod(fmod(theta, 2pi) + 2pi, 2pi)
+        float th = fmodf(y1[2], kTwoPi) + kTwoPi;
+        y1[2] = fmodf(th, kTwoPi);
+    }
 }
 
 // Sample one initial condition: gym Box.sample (uniform in [low, high], float32),
@@ -774,7 +982,7 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
 // branch between the two layouts made the waitcnt pass stall the wave on the state loads
 // before it issued the action load (two serial memory round trips).
 template <int MODEL, int INTEG, bool ASOA, int EPW = kWave>
-__global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state, const float* __restrict__ action,
+__global__ __launch_bounds__(kBlock) RR_STEP_ATTR void step_kernel(float* __restrict__ state, const float* __restrict__ action,
                                                       uint32_t n_envs, uint32_t mode, const KParams P, const Bufs B,
                                                       const StepIO io)
 {
@@ -797,6 +1005,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
     const uint32_t wave_idx = blockIdx.x * kWavesPerBlock + wv;
     const uint32_t wave_base = wave_idx * EPW;
     if (wave_base >= n) return;  // wave-uniform
+#if RR_STAGGER
+    {  // experiment: delay the load burst of some waves (group = wave in block, or block)
+        const uint32_t grp = (RR_STAGGER_BY == 0 ? wv : __builtin_amdgcn_readfirstlane(blockIdx.x / 8u)) % RR_STAGGER;
+        for (uint32_t k = 0; k < grp; ++k) __builtin_amdgcn_s_sleep(RR_STAGGER_SLEEP);
+    }
+#endif
     const uint32_t i = wave_base + lane;
     const bool valid = (EPW == kWave || lane < (uint32_t)EPW) && i < n;
     const uint32_t ic = valid ? i : n - 1;
@@ -888,18 +1102,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
 #endif
     RR_STAMP(3);
 
-    if constexpr (MODEL == 6) {
-        // _normalize_quaternion (simulator.py:250)
-        float rn = frsq(y1[6] * y1[6] + y1[7] * y1[7] + y1[8] * y1[8] + y1[9] * y1[9]);
-        y1[6] *= rn;
-        y1[7] *= rn;
-        y1[8] *= rn;
-        y1[9] *= rn;
-    } else {
-        // _wrapTo2Pi (simulator.py:150-163): fmod(fmod(theta, 2pi) + 2pi, 2pi)
-        float th = fmodf(y1[2], kTwoPi) + kTwoPi;
-        y1[2] = fmodf(th, kTwoPi);
-    }
+    post_integrate<MODEL>(y1);
 
     bool bv;
     float t[NT];
@@ -929,8 +1132,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
     RR_STAMP(4);
 
     float o[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) o[j] = y1[j] * H.inv_norm[j];
+    normalize_obs<NS>(y1, H.inv_norm, o);
 
     // Done compaction: one ballot per wave; lane 0 stores the wave's 64-bit done mask
     // (every wave writes its word each step, so no clearing and no atomics; the host
@@ -979,8 +1181,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
 #endif
             bst_f(st_r, v0, vo, v0_off);
             cw = ep << kEpisodeShift;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) o[j] = y1[j] * H.inv_norm[j];
+            normalize_obs<NS>(y1, H.inv_norm, o);
             el = 0;
             ret = 0.0f;
         }
@@ -1013,11 +1214,16 @@ __global__ __launch_bounds__(kBlock) void step_kernel(float* __restrict__ state,
     RR_STAMP(7);
     uint64_t rt1_;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1_)::"memory");
+    uint32_t xcc_, hwid_;  // placement of this wave
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid_));
     if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 10 + k] = stamp_[k];
-        B.stamps[(size_t)wave_idx * 10 + 8] = rt0_;
-        B.stamps[(size_t)wave_idx * 10 + 9] = rt1_;
+        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 12 + k] = stamp_[k];
+        B.stamps[(size_t)wave_idx * 12 + 8] = rt0_;
+        B.stamps[(size_t)wave_idx * 12 + 9] = rt1_;
+        B.stamps[(size_t)wave_idx * 12 + 10] = xcc_;
+        B.stamps[(size_t)wave_idx * 12 + 11] = hwid_;
     }
 #endif
 }
@@ -1322,7 +1528,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
 #if RR_DIAG == 4
-        {(void**)&e->stamps, sizeof(uint64_t) * 10 * n_words(n)},
+        {(void**)&e->stamps, sizeof(uint64_t) * 12 * n_words(n)},
 #endif
     };
     const bool exact = p->integrator == RR_INT_DOPRI5;
@@ -1810,9 +2016,9 @@ int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, cons
 // diagnostic build only: copy the per-wave phase stamps of the last step to the host
 int64_t rr_debug_stamps(rr_env* e, uint64_t* host, int64_t cap)
 {
-    const int64_t nw = std::min<int64_t>(cap / 10, n_words(e->n));
+    const int64_t nw = std::min<int64_t>(cap / 12, n_words(e->n));
     hipError_t err = hipDeviceSynchronize();
-    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 10 * nw, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 12 * nw, hipMemcpyDeviceToHost);
     return err == hipSuccess ? nw : hip_fail(err, "rr_debug_stamps");
 }
 #endif

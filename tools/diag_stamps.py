@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "diag"))
+    ap.add_argument("--graph", action="store_true", help="replay the steps back to back from a hipGraph")
+    ap.add_argument("--raw", help="save every sampled wave record (npz) for offline analysis")
     a = ap.parse_args()
     from rl_rocket_amd import build as b
 
@@ -46,13 +48,32 @@ def main():
     g = torch.Generator(device="cuda:0")
     g.manual_seed(3)
     nw = (a.n + 63) // 64
-    buf = np.zeros(nw * 10, np.uint64)
+    buf = np.zeros(nw * 12, np.uint64)
     rows = []
-    for k in range(a.steps):
-        env.step(torch.rand((a.n, 3), device="cuda:0", generator=g) * 2 - 1)
-        if k >= a.steps - 10:
-            lib.rr_debug_stamps(env._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
-            rows.append(buf.reshape(nw, 10).astype(np.int64).copy())
+    pool = [torch.rand((a.n, 3), device="cuda:0", generator=g) * 2 - 1 for _ in range(8)]
+    if a.graph:
+        for k in range(30):
+            env.step(pool[k % 8])
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                for k in range(16):
+                    env.step(pool[k % 8])
+        torch.cuda.current_stream().wait_stream(s)
+        for k in range(a.steps):
+            graph.replay()
+            if k >= a.steps - 10:  # stamps of the last step of the replay (after 15 back-to-back launches)
+                lib.rr_debug_stamps(env._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+                rows.append(buf.reshape(nw, 12).astype(np.int64).copy())
+    else:
+        for k in range(a.steps):
+            env.step(pool[k % 8])
+            if k >= a.steps - 10:
+                lib.rr_debug_stamps(env._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+                rows.append(buf.reshape(nw, 12).astype(np.int64).copy())
     allst = np.concatenate(rows)
     st = allst[:, :8]
     names = ["load", "rk4", "event", "reward", "done+reset", "store_issue", "store_drain"]
@@ -61,7 +82,9 @@ def main():
     for j, nm in enumerate(names):
         out[nm] = {"median": float(np.median(d[:, j])), "p90": float(np.percentile(d[:, j], 90)),
                    "max": float(d[:, j].max())}
-    per = allst.reshape(len(rows), nw, 10)
+    per = allst.reshape(len(rows), nw, 12)
+    if a.raw:
+        np.savez_compressed(a.raw, stamps=per)
     # realtime stamps: 100 MHz, one clock for every XCD -> dispatch skew and tail in us
     rt = [(p[:, 8] - p[:, 8].min()) / 100.0 for p in per]
     rte = [(p[:, 9] - p[:, 8].min()) / 100.0 for p in per]
