@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -81,6 +82,9 @@ namespace {
 #endif
 #ifndef RR_STEP_ATTR  // occupancy floor of the step kernel: <= 128 VGPRs keeps 4 waves per SIMD at large N
 #define RR_STEP_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+#ifndef RR_HELP_MAX_N  // largest N stepped with helper waves (step_kernel<..., HELP = true>)
+#define RR_HELP_MAX_N 131072
 #endif
 #ifndef RR_BLOCK
 #define RR_BLOCK 256
@@ -981,13 +985,21 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
 // ASOA: action layout [NA][N] (RR_FLAG_ACTION_SOA) as a template parameter: a runtime
 // branch between the two layouts made the waitcnt pass stall the wave on the state loads
 // before it issued the action load (two serial memory round trips).
-template <int MODEL, int INTEG, bool ASOA, int EPW = kWave>
-__global__ __launch_bounds__(kBlock) RR_STEP_ATTR void step_kernel(float* __restrict__ state, const float* __restrict__ action,
-                                                      uint32_t n_envs, uint32_t mode, const KParams P, const Bufs B,
-                                                      const StepIO io)
+template <int MODEL, int INTEG, bool ASOA, bool HELP = false, int EPW = kWave>
+__global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_kernel(
+    float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
+    const Bufs B, const StepIO io)
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][EPW * NS];
+    // HELP: the auto-reset candidates of main wave k are drawn by helper wave k + 4 of the
+    // same workgroup (on the same SIMD) into cand[k] (row per lane: NS values, v0, pad),
+    // published by cflag[k]. A lone wave issues one VALU op per 4 cycles and its SIMD can
+    // take one per 2, so the helper's ~190 instructions run beside the main wave's instead
+    // of before them (they need the counter word, which arrives with the state planes).
+    constexpr int kCandRow = (NS + 1 + 3) / 4 * 4;
+    __shared__ __attribute__((aligned(16))) float cand[HELP ? kWavesPerBlock : 1][HELP ? kWave * kCandRow : 1];
+    __shared__ uint32_t cflag[kWavesPerBlock];
 #if RR_DIAG == 7
     return;  // launch + dispatch floor
 #endif
@@ -1002,6 +1014,27 @@ __global__ __launch_bounds__(kBlock) RR_STEP_ATTR void step_kernel(float* __rest
     // uniform, and every buffer store with a wave_base soffset became a waterfall loop
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t n = n_envs;
+    if constexpr (HELP) {
+        if (wv < (uint32_t)kWavesPerBlock && lane == 0) cflag[wv] = 0u;
+        __syncthreads();  // flags cleared before any helper can publish
+        if (wv >= (uint32_t)kWavesPerBlock) {
+            const uint32_t k = wv - kWavesPerBlock;  // the main wave this helper serves
+            const uint32_t base = (blockIdx.x * kWavesPerBlock + k) * EPW;
+            if ((mode & RR_FLAG_AUTO_RESET) && base < n) {
+                const uint32_t ih = min(base + lane, n - 1);
+                const uint32_t cwh = (mode & kModeCounter) ? at(B.counter, ih) : 0u;
+                float s_[NS], v_;
+                ResetStream key = reset_stream(P.seed_w, P.id_off + base + lane, cwh);
+                sample_ic<MODEL>(P, key, s_, v_);
+                float* row = &cand[k][lane * kCandRow];
+#pragma unroll
+                for (int j = 0; j < NS; ++j) row[j] = s_[j];
+                row[NS] = v_;
+            }
+            __hip_atomic_store(&cflag[k], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+    }
     const uint32_t wave_idx = blockIdx.x * kWavesPerBlock + wv;
     const uint32_t wave_base = wave_idx * EPW;
     if (wave_base >= n) return;  // wave-uniform
@@ -1056,20 +1089,13 @@ __global__ __launch_bounds__(kBlock) RR_STEP_ATTR void step_kernel(float* __rest
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
 #if RR_EARLY_RESET
-    // SB3 auto-reset candidate of this step, keyed on (gid, counter word): ~200 VALU that
-    // fill the wait for the state planes instead of lengthening the done branch of the
-    // waves that finish last (RR_DIAG=4 stamps: 1560 cycles). Used by done lanes only.
+    // SB3 auto-reset candidate of this step, keyed on (gid, counter word): ~190 VALU right
+    // after the counter word lands, instead of in the done branch of the waves that finish
+    // last. Used by done lanes only. (HELP: drawn by the helper wave instead.)
     float ic_s[NS], ic_v0 = 0.0f;
-    if (mode & RR_FLAG_AUTO_RESET) {
+    if (!HELP && (mode & RR_FLAG_AUTO_RESET)) {
         ResetStream key = reset_stream(P.seed_w, P.id_off + i, cw);
         sample_ic<MODEL>(P, key, ic_s, ic_v0);
-#if RR_EARLY_RESET == 2
-        // park the candidate in this wave's (still unused) obs-tile LDS, plane-major so the
-        // accesses are bank-conflict free; it is read back only by lanes that reset
-#pragma unroll
-        for (int j = 0; j < NS; ++j)
-            if (lane < (uint32_t)EPW) lds[wv][j * EPW + lane] = ic_s[j];
-#endif
     }
 #endif
 #if RR_DIAG == 4
@@ -1167,11 +1193,15 @@ __global__ __launch_bounds__(kBlock) RR_STEP_ATTR void step_kernel(float* __rest
         }
         if ((mode & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
-#if RR_EARLY_RESET == 2
+            if constexpr (HELP) {
+                while (__hip_atomic_load(&cflag[wv], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+                    __builtin_amdgcn_s_sleep(1);
+                const float* row = &cand[wv][lane * kCandRow];
 #pragma unroll
-            for (int j = 0; j < NS; ++j) y1[j] = lds[wv][j * EPW + lane];
-            v0 = MODEL == 6 ? fsqrt(y1[3] * y1[3] + y1[4] * y1[4] + y1[5] * y1[5]) : fsqrt(y1[3] * y1[3] + y1[4] * y1[4]);
-#elif RR_EARLY_RESET
+                for (int j = 0; j < NS; ++j) y1[j] = row[j];
+                v0 = row[NS];
+            } else {
+#if RR_EARLY_RESET
 #pragma unroll
             for (int j = 0; j < NS; ++j) y1[j] = ic_s[j];
             v0 = ic_v0;
@@ -1179,6 +1209,7 @@ __global__ __launch_bounds__(kBlock) RR_STEP_ATTR void step_kernel(float* __rest
             ResetStream key = reset_stream(P.seed_w, P.id_off + i, cw);
             sample_ic<MODEL>(P, key, y1, v0);
 #endif
+            }
             bst_f(st_r, v0, vo, v0_off);
             cw = ep << kEpisodeShift;
             normalize_obs<NS>(y1, H.inv_norm, o);
@@ -1429,6 +1460,7 @@ struct rr_env {
     int ns, na, nt;
     int64_t n, id_off;
     uint64_t steps;
+    int64_t help_max_n;       // largest N stepped with helper waves (RR_HELP_MAX_N, env override)
     float* state;
     float* v0;
     uint32_t* counter;
@@ -1516,6 +1548,11 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->nt = p->model == RR_MODEL_6DOF ? 5 : 6;
     e->n = n;
     e->id_off = env_id_offset;
+    {
+        // test / A-B override of the helper-wave threshold: RR_HELP_MAX_N=<n> in the environment
+        const char* hv = std::getenv("RR_HELP_MAX_N");
+        e->help_max_n = hv ? std::strtoll(hv, nullptr, 10) : (int64_t)RR_HELP_MAX_N;
+    }
     DeviceGuard g(device);
     struct A {
         void** ptr;
@@ -1634,8 +1671,17 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
         const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
         const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
         const bool soa = e->p.flags & RR_FLAG_ACTION_SOA;
-#define RR_LAUNCH(M, I, A) \
-    hipLaunchKernelGGL((step_kernel<M, I, A>), grid, block, 0, s, e->state, action, nn, mode, e->kp, b, io)
+        // small N (at most ~2 main waves per SIMD): helper waves draw the reset candidates
+        const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;
+#define RR_LAUNCH(M, I, A)                                                                                       \
+    do {                                                                                                          \
+        if (help)                                                                                                 \
+            hipLaunchKernelGGL((step_kernel<M, I, A, true>), grid, dim3(2 * kBlock), 0, s, e->state, action, nn, \
+                               mode, e->kp, b, io);                                                               \
+        else                                                                                                      \
+            hipLaunchKernelGGL((step_kernel<M, I, A, false>), grid, block, 0, s, e->state, action, nn, mode,     \
+                               e->kp, b, io);                                                                     \
+    } while (0)
         if (m6 && !euler) {
             if (soa) RR_LAUNCH(6, RR_INT_RK4, true);
             else RR_LAUNCH(6, RR_INT_RK4, false);

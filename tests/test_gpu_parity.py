@@ -159,3 +159,43 @@ def test_full_size_properties_6dof():
     cfg = config_6dof(**kw)
     obs = h1[-1][0].cpu().numpy()
     np.testing.assert_allclose(obs, (st.T / cfg.state_normalizer).astype(np.float32), rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", [6, 3])
+def test_helper_wave_launch_is_bitwise_equal(model, monkeypatch):
+    """At small N the step kernel runs with helper waves that draw the auto-reset candidates
+    (step_kernel<..., HELP = true>, rr_create reads RR_HELP_MAX_N). Outputs, terminal rows
+    and state must be bitwise those of the single-role kernel, over steps with many resets."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 65536 + 300  # ragged last workgroup
+    kw = _env6() if model == 6 else {}
+
+    def run(help_max_n):
+        monkeypatch.setenv("RR_HELP_MAX_N", str(help_max_n))
+        b = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=40, **kw)
+        b.reset()
+        gen = torch.Generator(device="cuda:0")
+        gen.manual_seed(7)
+        out, resets = [], 0
+        for _ in range(60):
+            a = torch.rand((n, b.action_dim), device="cuda:0", generator=gen) * 2 - 1
+            obs, rew, done, trunc = b.step(a)
+            idx, tobs, ret, ln = b.fetch_done()
+            resets += len(idx)
+            out.append((obs.clone(), rew.clone(), done.clone(), trunc.clone(), torch.as_tensor(tobs).clone()))
+        st = b.get_state()
+        torch.cuda.synchronize()
+        b.close()
+        return out, st, resets
+
+    h_help, st_help, resets = run(1 << 40)
+    h_plain, st_plain, _ = run(0)
+    assert resets >= n  # TimeLimit 40 over 60 steps: every env reset at least once
+    for x, y in zip(h_help, h_plain):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+    for u, v in zip(st_help, st_plain):
+        assert torch.equal(torch.as_tensor(u), torch.as_tensor(v))
