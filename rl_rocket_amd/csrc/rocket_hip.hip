@@ -34,7 +34,7 @@
 //   3 = compute only (state synthesised in registers instead of loaded),
 //   4 = product kernel + s_memtime phase stamps per wave (rr_debug_stamps),
 //   5 = no event path, 6 = no in-kernel reset, 7 = empty kernel (launch + dispatch floor),
-//   8 = empty kernel allocating RR_DIAG8_V + 1 VGPRs.
+//   8 = empty kernel allocating RR_DIAG8_V + 1 VGPRs, 9 = reward terms skipped (bounds kept).
 #ifndef RR_DIAG
 #define RR_DIAG 0
 #endif
@@ -856,6 +856,20 @@ __device__ __forceinline__ void sample_ic(const KParams& P, ResetStream& k, floa
     }
 }
 
+// Bounds violation on the float32 post-step state: 6DOF Box(lo, hi, float32).contains(r)
+// (rocket_env.py:1036-1038, inclusive); 3DOF _check_bounds (rocket_env.py:431-447).
+template <int MODEL>
+__device__ __forceinline__ bool bounds_hit(const HotParams& P, const float* s)
+{
+    if constexpr (MODEL == 6) {
+        const bool inside = (s[0] >= P.blo[0]) & (s[0] <= P.bhi[0]) & (s[1] >= P.blo[1]) & (s[1] <= P.bhi[1]) &
+                            (s[2] >= P.blo[2]) & (s[2] <= P.bhi[2]);
+        return !inside;
+    } else {
+        return (s[0] <= P.blo[0]) | (s[0] >= P.bhi[0]) | (s[1] >= P.bhi[1]);
+    }
+}
+
 // Reward / done of the reference env on the float32 post-step state.
 template <int MODEL>
 __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s, const float* a, float v0,
@@ -865,10 +879,7 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
     // cases with selects, so a lone wave runs straight-line code (short-circuit && / ||
     // compiled to ~8 exec-mask branches here).
     if constexpr (MODEL == 6) {
-        // _check_bounds_violation: Box(lo, hi, float32).contains(r) (rocket_env.py:1036-1038)
-        const bool inside = (s[0] >= P.blo[0]) & (s[0] <= P.bhi[0]) & (s[1] >= P.blo[1]) & (s[1] <= P.bhi[1]) &
-                            (s[2] >= P.blo[2]) & (s[2] <= P.bhi[2]);
-        bounds_violation = !inside;
+        bounds_violation = bounds_hit<6>(P, s);
         // _compute_vtarg (rocket_env.py:986-1014)
         const bool above = s[0] > P.waypoint;
         const float rh0 = above ? s[0] - P.waypoint : s[0] + 1.0f;
@@ -910,8 +921,7 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         if (P.flags & RR_FLAG_REWARD_ANNEALING) return t[3] + t[4] - P.xi * (a[2] + 1.0f);
         return t[0] + t[1] + t[2] + t[3] + t[4] + (bounds_violation ? -50.0f : 0.0f);
     } else {
-        // _check_bounds (rocket_env.py:431-447)
-        bounds_violation = (s[0] <= P.blo[0]) | (s[0] >= P.bhi[0]) | (s[1] >= P.bhi[1]);
+        bounds_violation = bounds_hit<3>(P, s);
         // _compute_vtarg (rocket_env.py:219-247)
         const bool above = s[1] > P.waypoint;
         const float rh0 = above ? s[0] : 0.0f;
@@ -1137,6 +1147,11 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
 #pragma unroll
     for (int j = 0; j < NT; ++j) t[j] = 0.0f;
     float r = v0;
+#elif RR_DIAG == 9  // reward terms skipped (bounds kept): the reward's share of the launch
+    bv = bounds_hit<MODEL>(H, y1);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) t[j] = 0.0f;
+    float r = v0 + a[0];
 #else
     float r = reward_terms<MODEL>(H, y1, a, v0, bv, t);
 #endif
