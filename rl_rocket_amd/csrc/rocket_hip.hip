@@ -1189,7 +1189,7 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
             // row i of [N][NS]: 16-B stores (rows are 4-B aligned; gfx950 buffer stores
             // need only dword alignment), NS = 14 -> 3 x 16 B + 8 B, NS = 7 -> 16 B + 12 B
             const rsrc_t tr = make_rsrc(B.term_obs, (uint64_t)NS * plane);
-            const uint32_t ro = i * (NS * 4u);
+            const uint32_t ro = NS == 14 ? (i << 6) - (i << 3) : i * (NS * 4u);  // i * 56 without v_mul_lo_u32
             auto u4 = [&](int j) {
                 return u32x4{__float_as_uint(o[j]), __float_as_uint(o[j + 1]), __float_as_uint(o[j + 2]),
                              __float_as_uint(o[j + 3])};
@@ -1203,8 +1203,8 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
                 __builtin_amdgcn_raw_buffer_store_b96(
                     u32x3{__float_as_uint(o[NS - 3]), __float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
                     (int)(ro + (NS - 3) * 4), 0, 0);
-            B.term_ret[i] = ret;
-            B.term_len[i] = el;
+            bst_f<0>(make_rsrc(B.term_ret, plane), ret, vo, 0);
+            bst_u<0>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
         }
         if ((mode & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
             const uint32_t ep = (cw >> kEpisodeShift) + 1u;
