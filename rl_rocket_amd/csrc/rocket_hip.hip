@@ -585,17 +585,23 @@ __device__ __forceinline__ void normalize_obs(const float* y, const float* inv_n
 #endif
 }
 
-__device__ __forceinline__ void integrate6_rk4_pk(const KParams& P, const Ctl& c, const float* y0, float* y1,
-                                                  float* f0)
-{
-    const float h = P.h, hh = P.h2, h6 = P.h6, hh6 = P.h * P.h6;
-    const f2 t2xy = {2.0f * c.tbx, 2.0f * c.tby};
-    const float t2z = 2.0f * c.tbz;
-    const f2 tbxy = {c.tbx, c.tby};
-    const f2 t2zn = {t2z, -t2z}, t2yx = {-t2xy.y, t2xy.x};
-    const f2 gxy = {-kG0, 0.0f};
-    // R(q) T_b / m + g with the unnormalised q (see rhs): pair (ax, ay) and az
-    auto accel = [&](f2 q01, f2 q23, float m, f2& axy, float& az) {
+// Packed 6DOF RHS pieces for one step's controls: R(q) T_b / m + g as (ax, ay), az, and
+// dq = Omega(W) q with W = w / 2 (pairs (q0,q1), (q2,q3); see rhs for the formulas).
+struct Pk6 {
+    f2 t2xy, tbxy, t2zn, t2yx, gxy;
+    float t2z, tbz;
+    __device__ __forceinline__ explicit Pk6(const Ctl& c)
+    {
+        t2xy = f2{2.0f * c.tbx, 2.0f * c.tby};
+        t2z = 2.0f * c.tbz;
+        tbxy = f2{c.tbx, c.tby};
+        tbz = c.tbz;
+        t2zn = f2{t2z, -t2z};
+        t2yx = f2{-t2xy.y, t2xy.x};
+        gxy = f2{-kG0, 0.0f};
+    }
+    __device__ __forceinline__ void accel(f2 q01, f2 q23, float m, f2& axy, float& az) const
+    {
         const f2 sq = pk_fma(q01, q01, q23 * q23);
         const float qq = sq.x + sq.y;
         // t = 2 u x T_b, u = (q1, q2, q3), with qa = (q2, q1):
@@ -607,25 +613,65 @@ __device__ __forceinline__ void integrate6_rk4_pk(const KParams& P, const Ctl& c
         // F = |q|^2 T_b + q0 t + u x t;  (u x t)_xy = qa (tz, -tz) + q3 (-ty, tx)
         const f2 uxt = pk_fma(qa, f2{tz, -tz}, q3 * (pk_swap(txy) * f2{-1.0f, 1.0f}));
         const f2 Fxy = pk_fma(pk_bc(qq), tbxy, pk_fma(pk_lo(q01), txy, uxt));
-        const float Fz = fmaf(qq, c.tbz, fmaf(q01.x, tz, fmaf(q01.y, txy.y, -q23.x * txy.x)));
+        const float Fz = fmaf(qq, tbz, fmaf(q01.x, tz, fmaf(q01.y, txy.y, -q23.x * txy.x)));
         const float sc = frcp(qq * m);
         axy = pk_fma(Fxy, pk_bc(sc), gxy);
         az = Fz * sc;
-    };
+    }
+    // dq = Omega(W) q:
+    //   (d0, d1) = (-W1, W1) (q1, q0) + (-W2, W3) (q2, q2) - (W3, W2) (q3, q3)
+    //   (d2, d3) = (W2, W3) (q0, q0) + (-W3, W2) (q1, q1) + (W1, -W1) (q3, q2)
+    static __device__ __forceinline__ void dq(f2 q01, f2 q23, float W1, f2 W, f2& d01, f2& d23)
+    {
+        const f2 w1a = {-W1, W1}, w1b = {W1, -W1};
+        const f2 Wn = W * f2{-1.0f, 1.0f}, Ws = pk_swap(W), Wsn = Ws * f2{-1.0f, 1.0f};
+        d01 = pk_fma(w1a, pk_swap(q01), pk_fma(Wn, pk_lo(q23), -(Ws * pk_hi(q23))));
+        d23 = pk_fma(W, pk_lo(q01), pk_fma(Wsn, pk_hi(q01), w1b * pk_swap(q23)));
+    }
+};
+
+// Full 6DOF RHS f(s) on the packed pieces (the ground-event path's f(y1)).
+__device__ __forceinline__ void rhs6_pk(const Ctl& c, const float* s, float* d)
+{
+    const Pk6 k(c);
+    f2 axy, d01, d23;
+    float az;
+    const f2 q01 = {s[6], s[7]}, q23 = {s[8], s[9]};
+    k.accel(q01, q23, s[13], axy, az);
+    const float W1 = 0.5f * s[10];
+    const f2 W = {0.5f * s[11], 0.5f * s[12]};
+    Pk6::dq(q01, q23, W1, W, d01, d23);
+    const f2 A = {c.tau1, c.tau2};
+    const f2 B = {(-kJd1 * kJinv2) * s[10], (-kJd2 * kJinv3) * s[10]};
+    const f2 dw = pk_fma(B, f2{s[12], s[11]}, A);
+    d[0] = s[3];
+    d[1] = s[4];
+    d[2] = s[5];
+    d[3] = axy.x;
+    d[4] = axy.y;
+    d[5] = az;
+    d[6] = d01.x;
+    d[7] = d01.y;
+    d[8] = d23.x;
+    d[9] = d23.y;
+    d[10] = 0.0f;
+    d[11] = dw.x;
+    d[12] = dw.y;
+    d[13] = c.dm;
+}
+
+__device__ __forceinline__ void integrate6_rk4_pk(const KParams& P, const Ctl& c, const float* y0, float* y1,
+                                                  float* f0)
+{
+    const float h = P.h, hh = P.h2, h6 = P.h6, hh6 = P.h * P.h6;
+    const Pk6 k(c);
+    auto accel = [&](f2 q01, f2 q23, float m, f2& axy, float& az) { k.accel(q01, q23, m, axy, az); };
     const float W1 = 0.5f * y0[10];
     // dW2 = A2 + B2 W3, dW3 = A3 + B3 W2 (half of dw = J^-1 (tau - w x Jw)): pair form
     // dW = A + B swap(W)
     const f2 A = {0.5f * c.tau1, 0.5f * c.tau2};
     const f2 B = {(-2.0f * kJd1 * kJinv2) * W1, (-2.0f * kJd2 * kJinv3) * W1};
-    // dq = Omega(W) q:
-    //   (d0, d1) = (-W1, W1) (q1, q0) + (-W2, W3) (q2, q2) - (W3, W2) (q3, q3)
-    //   (d2, d3) = (W2, W3) (q0, q0) + (-W3, W2) (q1, q1) + (W1, -W1) (q3, q2)
-    const f2 w1a = {-W1, W1}, w1b = {W1, -W1};
-    auto dq = [&](f2 q01, f2 q23, f2 W, f2& d01, f2& d23) {
-        const f2 Wn = W * f2{-1.0f, 1.0f}, Ws = pk_swap(W), Wsn = Ws * f2{-1.0f, 1.0f};
-        d01 = pk_fma(w1a, pk_swap(q01), pk_fma(Wn, pk_lo(q23), -(Ws * pk_hi(q23))));
-        d23 = pk_fma(W, pk_lo(q01), pk_fma(Wsn, pk_hi(q01), w1b * pk_swap(q23)));
-    };
+    auto dq = [&](f2 q01, f2 q23, f2 W, f2& d01, f2& d23) { Pk6::dq(q01, q23, W1, W, d01, d23); };
     const f2 q01 = {y0[6], y0[7]}, q23 = {y0[8], y0[9]};
     const f2 W0 = {0.5f * y0[11], 0.5f * y0[12]};
     const float m0 = y0[13];
@@ -763,10 +809,14 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
     constexpr int NS = Dims<MODEL>::NS;
     const float x0 = y0[EV], x1 = y1[EV];
     if (x1 == 0.0f) return;  // root at the step end: state unchanged
-    float s = 0.0f;
     float f1[NS];
-    rhs<MODEL>(P, c, y1, f1);
-    if (x0 != 0.0f) {
+    if constexpr (MODEL == 6) rhs6_pk(c, y1, f1);
+    else rhs<MODEL>(P, c, y1, f1);
+    // straight-line code (one basic block with the RHS, so the scheduler interleaves the
+    // two): x0 == 0 gives the secant guess 0 and H(0) == 0, so s stays 0 (y = y0, as the
+    // reference's root at the step start)
+    float s;
+    {
         const float hv0 = P.h * f0[EV], hv1 = P.h * f1[EV];
         // the altitude's Hermite cubic in monomial form: H(s) = ((c3 s + c2) s + c1) s + c0
         const float dx = x1 - x0;
