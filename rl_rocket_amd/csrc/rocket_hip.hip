@@ -34,7 +34,8 @@
 //   3 = compute only (state synthesised in registers instead of loaded),
 //   4 = product kernel + s_memtime phase stamps per wave (rr_debug_stamps),
 //   5 = no event path, 6 = no in-kernel reset, 7 = empty kernel (launch + dispatch floor),
-//   8 = empty kernel allocating RR_DIAG8_V + 1 VGPRs, 9 = reward terms skipped (bounds kept).
+//   8 = empty kernel allocating RR_DIAG8_V + 1 VGPRs, 9 = reward terms skipped (bounds kept),
+//   10 = v0 not loaded, 11 = action not loaded (timing probes).
 #ifndef RR_DIAG
 #define RR_DIAG 0
 #endif
@@ -1128,6 +1129,10 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
     if constexpr (ASOA) {
 #pragma unroll
         for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
+    } else if constexpr (NA == 3 && RR_DIAG == 11) {  // action not loaded (timing probe)
+        a[0] = 0.1f * (float)(lane & 3);
+        a[1] = -0.1f;
+        a[2] = 0.3f;
     } else if constexpr (NA == 3) {
         const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)((vo << 1) + vo), 0, RR_LD_AUX);  // 12 B rows
         a[0] = __uint_as_float(v.x);
@@ -1145,7 +1150,11 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
 #pragma unroll
     for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
 #endif
+#if RR_DIAG == 10  // v0 not loaded (timing probe: is the last load's arrival critical?)
+    float v0 = 50.0f + (float)(lane & 7);
+#else
     float v0 = bld_f(st_r, vo, v0_off);
+#endif
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
 #if RR_EARLY_RESET
