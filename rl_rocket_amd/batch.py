@@ -20,7 +20,7 @@ def _ptr(t):
 class RocketBatch:
     def __init__(self, num_envs, model="6DOF", device=None, max_episode_steps=0, auto_reset=True,
                  episode_stats=True, reward_annealing=False, integrator="rk4", env_id_offset=0,
-                 compute_terms=False, seed=None, scipy_h0_clamp=False, **env_kwargs):
+                 compute_terms=False, seed=None, scipy_h0_clamp=False, action_soa=False, **env_kwargs):
         import torch
 
         self.torch = torch
@@ -40,7 +40,9 @@ class RocketBatch:
         self.n_terms = len(self.cfg.term_names)
         self.params = lower(self.cfg, max_episode_steps=max_episode_steps, auto_reset=auto_reset,
                             episode_stats=episode_stats, reward_annealing=reward_annealing, integrator=integrator,
-                            scipy_h0_clamp=scipy_h0_clamp)
+                            scipy_h0_clamp=scipy_h0_clamp, action_soa=action_soa)
+        # action_soa: step() takes actions as [action_dim][N] planes (RR_FLAG_ACTION_SOA)
+        self.action_soa = bool(action_soa)
         self.lib = _lib.load()
         h = ctypes.c_void_p()
         _lib.check(self.lib.rr_create(ctypes.byref(h), ctypes.byref(self.params), self.num_envs, int(env_id_offset),
@@ -68,7 +70,7 @@ class RocketBatch:
             action = action.to(self.device, non_blocking=True)
         if action.dtype != t.float32:
             action = action.float()
-        action = action.reshape(self.num_envs, self.action_dim)
+        action = action.reshape((self.action_dim, self.num_envs) if self.action_soa else (self.num_envs, self.action_dim))
         if not action.is_contiguous():
             action = action.contiguous()
         return action
