@@ -45,9 +45,10 @@ def parse():
                     help="step: the fused env step (headline); rollout: on-device PPO rollout "
                          "collection (MlpPolicy 64x64 forward + sample + env step + buffer), BASELINE configs[4]")
     ap.add_argument("--rollout-steps", type=int, default=16)
-    ap.add_argument("--policy-dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="rollout mode: fused policy towers on fp32 MFMA (SB3-exact, default) or bf16 MFMA "
-                         "with fp32 accumulation (opt-in)")
+    ap.add_argument("--policy-dtype", default="fp32", choices=["fp32", "fp16x3", "bf16"],
+                    help="rollout mode: fused policy towers on fp32 MFMA (SB3-exact, default), split-fp16 MFMA "
+                         "(fp16x3: operands as fp16 hi + lo, three MFMAs per k step, fp32-level accuracy) or bf16 "
+                         "MFMA with fp32 accumulation (opt-in)")
     ap.add_argument("--rollout-two-launch", action="store_true",
                     help="rollout mode: rr_policy_act + rr_step per step instead of the one-launch rr_rollout_step")
     ap.add_argument("--rollout-torch", action="store_true",

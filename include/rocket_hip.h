@@ -185,9 +185,12 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
  * precision: RR_POLICY_FP32 (default; v_mfma_f32_32x32x2_f32, exact fp32 products, the
  * SB3 policy's numbers to fp32 rounding) or RR_POLICY_BF16 (opt-in; v_mfma_f32_32x32x16_bf16
  * with fp32 accumulation: obs, the tower weights and the first hidden layer rounded to
- * bf16, everything else fp32). A packed buffer is specific to its precision. */
+ * bf16, everything else fp32) or RR_POLICY_FP16X3 (v_mfma_f32_32x32x16_f16 on operands split
+ * into two fp16 halves, three MFMAs per k step: ~2^-21 relative products, fp32-level
+ * results at ~5x the fp32 MFMA rate). A packed buffer is specific to its precision. */
 #define RR_POLICY_FP32 0
 #define RR_POLICY_BF16 1
+#define RR_POLICY_FP16X3 2
 
 /* Packed parameter buffer for rr_policy_*: returns its size in floats (or RR_EINVAL) and,
  * if off != NULL, the 12 section offsets {L1A, B1, L2A, B2, TOWER, PI, VF, HA, HV, HB, VB,

@@ -24,7 +24,7 @@ RR_FLAG_REWARD_ANNEALING = 0x4
 RR_FLAG_ACTION_SOA = 0x8
 RR_FLAG_SCIPY_H0_CLAMP = 0x10
 RR_MAX_STATE = 14
-RR_POLICY_FP32, RR_POLICY_BF16 = 0, 1
+RR_POLICY_FP32, RR_POLICY_BF16, RR_POLICY_FP16X3 = 0, 1, 2
 
 _d3 = ctypes.c_double * 3
 _f14 = ctypes.c_float * RR_MAX_STATE

@@ -1954,15 +1954,16 @@ struct PolCfg {
 template <class F>
 static bool pol_dispatch(int obs_dim, int act_dim, int precision, F&& f)
 {
-    if (precision != RR_POLICY_FP32 && precision != RR_POLICY_BF16) return false;
-    const bool bf = precision == RR_POLICY_BF16;
+    if (precision != RR_POLICY_FP32 && precision != RR_POLICY_BF16 && precision != RR_POLICY_FP16X3) return false;
     if (obs_dim == 14 && act_dim == 3) {
-        if (bf) f(PolCfg<14, 3, 1>{});
+        if (precision == RR_POLICY_BF16) f(PolCfg<14, 3, 1>{});
+        else if (precision == RR_POLICY_FP16X3) f(PolCfg<14, 3, 2>{});
         else f(PolCfg<14, 3, 0>{});
         return true;
     }
     if (obs_dim == 7 && act_dim == 2) {
-        if (bf) f(PolCfg<7, 2, 1>{});
+        if (precision == RR_POLICY_BF16) f(PolCfg<7, 2, 1>{});
+        else if (precision == RR_POLICY_FP16X3) f(PolCfg<7, 2, 2>{});
         else f(PolCfg<7, 2, 0>{});
         return true;
     }
@@ -1970,7 +1971,7 @@ static bool pol_dispatch(int obs_dim, int act_dim, int precision, F&& f)
 }
 
 #define RR_POL_UNSUPPORTED(fn) \
-    fail(RR_EINVAL, fn ": supported (obs_dim, act_dim) are (14, 3) and (7, 2), precision RR_POLICY_FP32 / RR_POLICY_BF16")
+    fail(RR_EINVAL, fn ": supported (obs_dim, act_dim) are (14, 3) and (7, 2), precision RR_POLICY_FP32 / RR_POLICY_BF16 / RR_POLICY_FP16X3")
 
 extern "C" {
 
@@ -2066,8 +2067,8 @@ int rr_rollout_step(rr_env* e, const float* params, int precision, uint64_t seed
         !reward || !done)
         return fail(RR_EINVAL, "rr_rollout_step: null argument");
     if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_rollout_step: params must be 16-B aligned");
-    if (precision != RR_POLICY_FP32 && precision != RR_POLICY_BF16)
-        return fail(RR_EINVAL, "rr_rollout_step: precision must be RR_POLICY_FP32 or RR_POLICY_BF16");
+    if (precision != RR_POLICY_FP32 && precision != RR_POLICY_BF16 && precision != RR_POLICY_FP16X3)
+        return fail(RR_EINVAL, "rr_rollout_step: precision must be RR_POLICY_FP32, RR_POLICY_BF16 or RR_POLICY_FP16X3");
     if (e->p.integrator == RR_INT_DOPRI5)
         return fail(RR_EINVAL, "rr_rollout_step: RR_INT_DOPRI5 envs step through rr_policy_act + rr_step");
     RolloutIO io;
@@ -2097,22 +2098,19 @@ int rr_rollout_step(rr_env* e, const float* params, int precision, uint64_t seed
     const dim3 grid((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock)), block(rol::kThreads);
     hipStream_t s = (hipStream_t)stream;
     const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
-    const bool bf = precision == RR_POLICY_BF16;
 #define RR_LAUNCH(M, I, PR) \
     hipLaunchKernelGGL((rollout_step_kernel<M, I, PR>), grid, block, 0, s, e->state, nn, mode, e->kp, b, io)
-    if (m6 && !euler) {
-        if (bf) RR_LAUNCH(6, RR_INT_RK4, 1);
-        else RR_LAUNCH(6, RR_INT_RK4, 0);
-    } else if (m6) {
-        if (bf) RR_LAUNCH(6, RR_INT_EULER, 1);
-        else RR_LAUNCH(6, RR_INT_EULER, 0);
-    } else if (!euler) {
-        if (bf) RR_LAUNCH(3, RR_INT_RK4, 1);
-        else RR_LAUNCH(3, RR_INT_RK4, 0);
-    } else {
-        if (bf) RR_LAUNCH(3, RR_INT_EULER, 1);
-        else RR_LAUNCH(3, RR_INT_EULER, 0);
-    }
+#define RR_LAUNCH_P(M, I)                                  \
+    do {                                                   \
+        if (precision == RR_POLICY_BF16) RR_LAUNCH(M, I, 1);     \
+        else if (precision == RR_POLICY_FP16X3) RR_LAUNCH(M, I, 2); \
+        else RR_LAUNCH(M, I, 0);                           \
+    } while (0)
+    if (m6 && !euler) RR_LAUNCH_P(6, RR_INT_RK4);
+    else if (m6) RR_LAUNCH_P(6, RR_INT_EULER);
+    else if (!euler) RR_LAUNCH_P(3, RR_INT_RK4);
+    else RR_LAUNCH_P(3, RR_INT_EULER);
+#undef RR_LAUNCH_P
 #undef RR_LAUNCH
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return hip_fail(err, "rr_rollout_step: launch");

@@ -16,7 +16,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 TOL = 2e-5
-PREC = {"fp32": 0, "bf16": 1}
+PREC = {"fp32": 0, "bf16": 1, "fp16x3": 2}
+EXACTISH = ("fp32", "fp16x3")  # checked against the fp32 PyTorch policy itself
 
 
 def _bf(t):
@@ -56,7 +57,7 @@ def _policy(ns, na, seed=0):
     return pol
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16x3"])
 @pytest.mark.parametrize("ns,na", [(14, 3), (7, 2)])
 def test_policy_act_matches_torch(ns, na, prec):
     import torch
@@ -81,8 +82,8 @@ def test_policy_act_matches_torch(ns, na, prec):
     with torch.no_grad():
         mean, v = pol(obs)
         std = pol.log_std.exp()
-    if prec == "fp32":
-        print("value err", (val - v).abs().max().item())
+    if prec in EXACTISH:
+        print(prec, "value err", (val - v).abs().max().item())
         assert (val - v).abs().max().item() < TOL
     else:
         print("bf16 vs fp32 policy: value", (val - v).abs().max().item())
@@ -94,7 +95,7 @@ def test_policy_act_matches_torch(ns, na, prec):
     ref_lp = (-0.5 * eps ** 2 - pol.log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
     lp_err = (lp - ref_lp).abs()
     # bf16: eps is recovered through the emulated mean, so a mean difference d shows as eps * d / std
-    assert lp_err.max().item() < (1e-4 if prec == "fp32" else 5e-2)
+    assert lp_err.max().item() < (1e-4 if prec in EXACTISH else 5e-2)
     if prec == "bf16":
         assert lp_err.quantile(0.99).item() < 1e-3
     e = eps.cpu().numpy()
@@ -120,14 +121,14 @@ def test_policy_act_matches_torch(ns, na, prec):
                                  _ptr(val), _ptr(lp), None, None, None, None, 0.0, None, None, None, None),
                "rr_policy_act")
     torch.cuda.synchronize()
-    if prec == "fp32":
+    if prec in EXACTISH:
         with torch.no_grad():
             assert (act - pol(obs)[0]).abs().max().item() < TOL
     else:
         _check_close(act, _emulated_bf16(pol, obs)[0], "bf16 mean")
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16x3"])
 @pytest.mark.parametrize("ns,na", [(14, 3), (7, 2)])
 def test_policy_pack_kernel_matches_reference(ns, na, prec):
     import torch
@@ -141,7 +142,7 @@ def test_policy_pack_kernel_matches_reference(ns, na, prec):
     assert torch.equal(out[:pk.size].view(torch.int32), ref[:pk.size].view(torch.int32))  # bitwise (bf16 RNE)
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16x3"])
 def test_policy_bootstrap_and_gae(prec):
     import torch
     from rl_rocket_amd import _lib
@@ -164,7 +165,7 @@ def test_policy_bootstrap_and_gae(prec):
                                        _ptr(obs), _ptr(vout), None), "rr_policy_bootstrap")
     torch.cuda.synchronize()
     with torch.no_grad():
-        if prec == "fp32":
+        if prec in EXACTISH:
             ref = rew + 0.99 * pol.value(tobs) * trunc.float()
             vref = pol.value(obs)
         else:
@@ -205,7 +206,7 @@ def test_policy_bootstrap_and_gae(prec):
     assert (ret - (ref_adv + v)).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("fused,prec", [(True, "fp32"), (False, "fp32"), (True, "bf16")])
+@pytest.mark.parametrize("fused,prec", [(True, "fp32"), (False, "fp32"), (True, "bf16"), (True, "fp16x3")])
 def test_fused_collect_matches_semantics(fused, prec):
     """A fused and an unfused rollout of the same policy share every deterministic output
     (value of each visited obs, buffer layout) and both are graph-capturable."""
@@ -220,7 +221,7 @@ def test_fused_collect_matches_semantics(fused, prec):
     ro = DeviceRollout(env, pol, n_steps=T, fused=fused, policy_dtype=prec)
     assert ro.fused == fused
     ro.collect()
-    if prec == "fp32":
+    if prec in EXACTISH:
         with torch.no_grad():
             v = pol.value(ro.obs.reshape(-1, 14)).reshape(T, n)
         assert (ro.values - v).abs().max().item() < TOL
@@ -243,7 +244,7 @@ def test_fused_collect_matches_semantics(fused, prec):
     env.close()
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16x3"])
 @pytest.mark.parametrize("model", [6, 3])
 def test_one_launch_rollout_bitwise_equals_two_launch(model, prec):
     """rr_rollout_step (policy + env step in one kernel) against rr_policy_act + rr_step:

@@ -111,5 +111,41 @@ def test_layout_rejects_unsupported_dims():
 
     lib = _lib.load(require_torch=False)
     assert lib.rr_policy_layout(10, 3, _lib.RR_POLICY_FP32, None) == _lib.RR_EINVAL
-    assert lib.rr_policy_layout(14, 3, 2, None) == _lib.RR_EINVAL  # unknown precision
+    assert lib.rr_policy_layout(14, 3, 3, None) == _lib.RR_EINVAL  # unknown precision
     assert lib.rr_policy_layout(14, 3, _lib.RR_POLICY_BF16, None) < lib.rr_policy_layout(14, 3, 0, None)
+
+
+@pytest.mark.parametrize("ns,na", [(14, 3), (7, 2)])
+def test_pack_reference_fp16x3_matches_layout(ns, na):
+    """split-fp16 tower sections: [hi, lo] fp16 planes of 2^8 W in the bf16 fragment order;
+    hi + lo reproduces 2^8 W to 2^-21 relative (22 significant bits), biases packed at the
+    2^16 accumulator scale."""
+    import torch
+    from rl_rocket_amd.rollout import MlpActorCritic, PolicyPack
+
+    torch.manual_seed(5)
+    pol = MlpActorCritic(ns, na)
+    with torch.no_grad():
+        for prm in pol.parameters():
+            prm.add_(0.3 * torch.randn_like(prm))
+    pk = PolicyPack(pol, ns, na, torch.device("cpu"), precision="fp16x3")
+    buf = pk.pack_reference()
+    o, kp1 = pk.off, (ns + 15) // 16
+    plane1, plane2 = 2 * kp1 * 64 * 4, 2048
+    assert o["B1"] == 2 * plane1 and o["B2"] - o["L2A"] == 2 * plane2
+    f16 = buf.view(torch.int32).numpy().view(np.float16).astype(np.float64)  # 2 halves per float, low first
+    for tw, net in ((o["PI"], pol.pi_net), (o["VF"], pol.vf_net)):
+        w1 = torch.nn.functional.pad(net[0].weight.detach(), (0, 16 * kp1 - ns)).double().numpy()
+        w2 = net[2].weight.detach().double().numpy()
+        hi1 = f16[2 * (tw + o["L1A"]): 2 * (tw + o["L1A"] + plane1)]
+        lo1 = f16[2 * (tw + o["L1A"] + plane1): 2 * (tw + o["L1A"] + 2 * plane1)]
+        hi2 = f16[2 * (tw + o["L2A"]): 2 * (tw + o["L2A"] + plane2)]
+        lo2 = f16[2 * (tw + o["L2A"] + plane2): 2 * (tw + o["L2A"] + 2 * plane2)]
+        ref1 = 256.0 * w1[pk.l1_i.numpy(), pk.l1_k.numpy()]
+        ref2 = 256.0 * w2[pk.l2_i.numpy(), pk.l2_k.numpy()]
+        for hi, lo, ref in ((hi1, lo1, ref1), (hi2, lo2, ref2)):
+            err = np.abs(hi + lo - ref) / np.maximum(np.abs(ref), 1e-3)
+            assert err.max() < 2.0 ** -20, err.max()
+            assert np.all(np.abs(lo) <= np.abs(hi) * 2.0 ** -10 + 2.0 ** -24)
+        b1 = buf[tw + o["B1"]: tw + o["B1"] + 64].numpy()
+        assert np.array_equal(b1, (net[0].bias.detach()[pk.b_i] * 65536.0).numpy())

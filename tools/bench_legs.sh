@@ -14,6 +14,7 @@ run() {  # name, args...
   if [ "$rc" -ne 0 ]; then tail -5 "$OUT/$name.err"; exit "$rc"; fi
 }
 run rollout_fp32 --mode rollout
+run rollout_fp16x3 --mode rollout --policy-dtype fp16x3
 run rollout_bf16 --mode rollout --policy-dtype bf16
 run rollout_2launch --mode rollout --rollout-two-launch
 run euler3_4096 --model 3DOF --integrator euler --n 4096
