@@ -39,6 +39,9 @@
 #ifndef RR_DIAG
 #define RR_DIAG 0
 #endif
+// per-wave stamp buffer (rr_debug_stamps): 4 = phase stamps, 12 = start / end only (no waits
+// inside the wave, so the wave runs the product code; records its event / done lane counts)
+#define RR_STAMPS (RR_DIAG == 4 || RR_DIAG == 12)
 
 namespace {
 
@@ -59,6 +62,9 @@ namespace {
 #endif
 #ifndef RR_NEWTON_ITERS
 #define RR_NEWTON_ITERS 3
+#endif
+#ifndef RR_EVENT_QSTART  // 1 = Newton starts at the quadratic's root instead of the secant (A/B)
+#define RR_EVENT_QSTART 0
 #endif
 #ifndef RR_LD_AUX
 #define RR_LD_AUX 0
@@ -86,6 +92,9 @@ namespace {
 #endif
 #ifndef RR_HELP_MAX_N  // largest N stepped with helper waves (step_kernel<..., HELP = true>)
 #define RR_HELP_MAX_N 131072
+#endif
+#ifndef RR_NARROW_MAX_N  // largest N stepped with one main wave per workgroup (helper variant)
+#define RR_NARROW_MAX_N 16384
 #endif
 #ifndef RR_BLOCK
 #define RR_BLOCK 256
@@ -215,7 +224,7 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
 }
 
 struct Bufs {
-#if RR_DIAG == 4
+#if RR_STAMPS
     uint64_t* stamps;         // [waves][12]: 8 s_memtime phase stamps, s_memrealtime at start / end, XCC_ID, HW_ID
 #endif
     float* state;
@@ -825,7 +834,20 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         const float d2 = 2.0f * c2, d3 = 3.0f * c3;
         const bool pos0 = x0 > 0.0f;
         float lo = 0.0f, hi = 1.0f;  // H(lo) has the sign of x0
+#if RR_EVENT_QSTART
+        // start at the root of the quadratic through x0 (slope hv0) and x1: Q(s) = x0 + hv0 s
+        // + (c2 + c3) s^2, stable form s = x0 / q, q = -(hv0 + sgn(hv0) sqrt(D)) / 2; Q changes
+        // sign on [0, 1], so D > 0 and the root lies in [0, 1]
+        {
+            const float aq = dx - hv0;  // c2 + c3
+            const float D = fmaxf(fmaf(hv0, hv0, -4.0f * aq * x0), 0.0f);
+            const float q = -0.5f * (hv0 + copysignf(fsqrt(D), hv0));
+            s = x0 * frcp(q);
+            s = (s >= 0.0f && s <= 1.0f) ? s : x0 * frcp(x0 - x1);  // (rounding guard: secant)
+        }
+#else
         s = x0 * frcp(x0 - x1);
+#endif
         // Newton from the secant guess, kept inside the closed sign bracket [lo, hi]
         // (bisection fallback). A converged iterate sits on a bracket end, so the test is
         // inclusive. Fixed 3 iterations, branch-free (quadratic convergence from the secant
@@ -1046,21 +1068,21 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
 // ASOA: action layout [NA][N] (RR_FLAG_ACTION_SOA) as a template parameter: a runtime
 // branch between the two layouts made the waitcnt pass stall the wave on the state loads
 // before it issued the action load (two serial memory round trips).
-template <int MODEL, int INTEG, bool ASOA, bool HELP = false, int EPW = kWave>
-__global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_kernel(
+template <int MODEL, int INTEG, bool ASOA, bool HELP = false, int WPB = kWavesPerBlock, int EPW = kWave>
+__global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR void step_kernel(
     float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
     const Bufs B, const StepIO io)
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
-    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][EPW * NS];
+    __shared__ __attribute__((aligned(16))) float lds[WPB][EPW * NS];
     // HELP: the auto-reset candidates of main wave k are drawn by helper wave k + 4 of the
     // same workgroup (on the same SIMD) into cand[k] (row per lane: NS values, v0, pad),
     // published by cflag[k]. A lone wave issues one VALU op per 4 cycles and its SIMD can
     // take one per 2, so the helper's ~190 instructions run beside the main wave's instead
     // of before them (they need the counter word, which arrives with the state planes).
     constexpr int kCandRow = (NS + 1 + 3) / 4 * 4;
-    __shared__ __attribute__((aligned(16))) float cand[HELP ? kWavesPerBlock : 1][HELP ? kWave * kCandRow : 1];
-    __shared__ uint32_t cflag[kWavesPerBlock];
+    __shared__ __attribute__((aligned(16))) float cand[HELP ? WPB : 1][HELP ? kWave * kCandRow : 1];
+    __shared__ uint32_t cflag[WPB];
 #if RR_DIAG == 7
     return;  // launch + dispatch floor
 #endif
@@ -1076,11 +1098,11 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t n = n_envs;
     if constexpr (HELP) {
-        if (wv < (uint32_t)kWavesPerBlock && lane == 0) cflag[wv] = 0u;
+        if (wv < (uint32_t)WPB && lane == 0) cflag[wv] = 0u;
         __syncthreads();  // flags cleared before any helper can publish
-        if (wv >= (uint32_t)kWavesPerBlock) {
-            const uint32_t k = wv - kWavesPerBlock;  // the main wave this helper serves
-            const uint32_t base = (blockIdx.x * kWavesPerBlock + k) * EPW;
+        if (wv >= (uint32_t)WPB) {
+            const uint32_t k = wv - WPB;  // the main wave this helper serves
+            const uint32_t base = (blockIdx.x * WPB + k) * EPW;
             if ((mode & RR_FLAG_AUTO_RESET) && base < n) {
                 const uint32_t ih = min(base + lane, n - 1);
                 const uint32_t cwh = (mode & kModeCounter) ? at(B.counter, ih) : 0u;
@@ -1096,7 +1118,7 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
             return;
         }
     }
-    const uint32_t wave_idx = blockIdx.x * kWavesPerBlock + wv;
+    const uint32_t wave_idx = blockIdx.x * WPB + wv;
     const uint32_t wave_base = wave_idx * EPW;
     if (wave_base >= n) return;  // wave-uniform
 #if RR_STAGGER
@@ -1116,8 +1138,8 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
     const rsrc_t st_r = make_rsrc(state, (uint64_t)(NS + 3) * plane);
     const rsrc_t act_r = make_rsrc(action, (uint64_t)NA * plane);
     const uint32_t v0_off = NS * plane, cw_off = (NS + 1) * plane, ret_off = (NS + 2) * plane;
-#if RR_DIAG == 4
-    uint64_t stamp_[8], rt0_;
+#if RR_STAMPS
+    uint64_t stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rt0_;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0_)::"memory");
 #endif
     RR_STAMP(0);
@@ -1314,7 +1336,11 @@ __global__ __launch_bounds__(HELP ? 2 * kBlock : kBlock) RR_STEP_ATTR void step_
     store_obs_tile<NS, EPW>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
                             io.obs_vec_ok);
     RR_STAMP(6);
-#if RR_DIAG == 4
+#if RR_DIAG == 12
+    stamp_[0] = __popcll(__ballot(event && valid));
+    stamp_[1] = __popcll(m);
+#endif
+#if RR_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     RR_STAMP(7);
     uint64_t rt1_;
@@ -1544,7 +1570,7 @@ struct rr_env {
     float* term_ret;
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
-#if RR_DIAG == 4
+#if RR_STAMPS
     uint64_t* stamps;
 #endif
     int32_t* g_idx;     // rr_fetch_done scratch
@@ -1563,7 +1589,7 @@ Bufs bufs_of(const rr_env* e)
     b.counter = e->counter;
     b.ep_ret = e->ep_ret;
     b.done_bits = e->done_bits;
-#if RR_DIAG == 4
+#if RR_STAMPS
     b.stamps = e->stamps;
 #endif
     b.term_obs = e->term_obs;
@@ -1638,7 +1664,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->term_ret, sizeof(float) * n},        {(void**)&e->term_len, sizeof(int32_t) * n},
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
-#if RR_DIAG == 4
+#if RR_STAMPS
         {(void**)&e->stamps, sizeof(uint64_t) * 12 * n_words(n)},
 #endif
     };
@@ -1747,14 +1773,20 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
         const bool soa = e->p.flags & RR_FLAG_ACTION_SOA;
         // small N (at most ~2 main waves per SIMD): helper waves draw the reset candidates
         const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;
-#define RR_LAUNCH(M, I, A)                                                                                       \
-    do {                                                                                                          \
-        if (help)                                                                                                 \
-            hipLaunchKernelGGL((step_kernel<M, I, A, true>), grid, dim3(2 * kBlock), 0, s, e->state, action, nn, \
-                               mode, e->kp, b, io);                                                               \
-        else                                                                                                      \
-            hipLaunchKernelGGL((step_kernel<M, I, A, false>), grid, block, 0, s, e->state, action, nn, mode,     \
-                               e->kp, b, io);                                                                     \
+        // up to 16 384 envs one main wave per workgroup (64 + 64 threads): the few workgroups
+        // spread over 4x as many CUs (A/B at N = 4 096: -5 % 6DOF); above, 4 main waves
+        const bool wide = e->n <= RR_NARROW_MAX_N;
+#define RR_LAUNCH(M, I, A)                                                                                          \
+    do {                                                                                                             \
+        if (help && wide)                                                                                            \
+            hipLaunchKernelGGL((step_kernel<M, I, A, true, 1>), dim3((unsigned)((e->n + kWave - 1) / kWave)),       \
+                               dim3(2 * kWave), 0, s, e->state, action, nn, mode, e->kp, b, io);                     \
+        else if (help)                                                                                               \
+            hipLaunchKernelGGL((step_kernel<M, I, A, true>), grid, dim3(2 * kBlock), 0, s, e->state, action, nn,    \
+                               mode, e->kp, b, io);                                                                  \
+        else                                                                                                         \
+            hipLaunchKernelGGL((step_kernel<M, I, A, false>), grid, block, 0, s, e->state, action, nn, mode,        \
+                               e->kp, b, io);                                                                        \
     } while (0)
         if (m6 && !euler) {
             if (soa) RR_LAUNCH(6, RR_INT_RK4, true);
@@ -2130,7 +2162,7 @@ int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, cons
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_gae: launch");
 }
 
-#if RR_DIAG == 4
+#if RR_STAMPS
 // diagnostic build only: copy the per-wave phase stamps of the last step to the host
 int64_t rr_debug_stamps(rr_env* e, uint64_t* host, int64_t cap)
 {

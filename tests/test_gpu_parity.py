@@ -163,14 +163,15 @@ def test_full_size_properties_6dof():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model", [6, 3])
-def test_helper_wave_launch_is_bitwise_equal(model, monkeypatch):
+@pytest.mark.parametrize("n", [65536 + 300, 4096 + 37])
+def test_helper_wave_launch_is_bitwise_equal(model, n, monkeypatch):
     """At small N the step kernel runs with helper waves that draw the auto-reset candidates
-    (step_kernel<..., HELP = true>, rr_create reads RR_HELP_MAX_N). Outputs, terminal rows
-    and state must be bitwise those of the single-role kernel, over steps with many resets."""
+    (step_kernel<..., HELP = true, WPB>, rr_create reads RR_HELP_MAX_N). Outputs, terminal
+    rows and state must be bitwise those of the single-role kernel, over steps with many
+    resets. Ragged last workgroup; N = 4096 + 37 runs one main wave per workgroup (WPB = 1)."""
     import torch
     from rl_rocket_amd.batch import RocketBatch
 
-    n = 65536 + 300  # ragged last workgroup
     kw = _env6() if model == 6 else {}
 
     def run(help_max_n):

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--model", type=int, default=6)
     ap.add_argument("--steps", type=int, default=4096)
+    ap.add_argument("--integrator", default="rk4")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "ab"))
     a = ap.parse_args()
     from rl_rocket_amd import build as b
@@ -47,7 +48,8 @@ def main():
             env = dict(os.environ, RR_LIB_PATH=lib)
             out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "diag_kernel.py"), "--child",
                                   "--tag", os.path.basename(src), "--n", str(a.n), "--model", str(a.model),
-                                  "--steps", str(a.steps)], env=env, capture_output=True, text=True, timeout=300)
+                                  "--steps", str(a.steps), "--integrator", a.integrator], env=env, capture_output=True,
+                                 text=True, timeout=300)
             if out.returncode != 0:
                 print(out.stderr[-2000:])
                 sys.exit(out.returncode)

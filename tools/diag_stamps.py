@@ -26,12 +26,16 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "diag"))
     ap.add_argument("--graph", action="store_true", help="replay the steps back to back from a hipGraph")
     ap.add_argument("--raw", help="save every sampled wave record (npz) for offline analysis")
+    ap.add_argument("--defines", default="", help="extra -D defines for the stamp build, comma separated")
+    ap.add_argument("--diag", type=int, default=4, choices=[4, 12],
+                    help="4: phase stamps (the waits serialise the wave); 12: start / end only (product code "
+                         "inside the wave; stamp slots 0 / 1 = event / done lanes of the wave)")
     a = ap.parse_args()
     from rl_rocket_amd import build as b
 
     os.makedirs(a.out, exist_ok=True)
-    lib_path = os.path.join(a.out, "librocket_hip_diag4.so")
-    subprocess.check_call(b.command(out=lib_path, defines=("RR_DIAG=4",)))
+    lib_path = os.path.join(a.out, "librocket_hip_diag%d.so" % a.diag)
+    subprocess.check_call(b.command(out=lib_path, defines=("RR_DIAG=%d" % a.diag,) + tuple(d for d in a.defines.split(",") if d)))
     os.environ["RR_LIB_PATH"] = lib_path
     import torch
 
