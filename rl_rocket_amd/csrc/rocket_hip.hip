@@ -63,9 +63,6 @@ namespace {
 #ifndef RR_NEWTON_ITERS
 #define RR_NEWTON_ITERS 3
 #endif
-#ifndef RR_EVENT_QSTART  // 1 = Newton starts at the quadratic's root instead of the secant (A/B)
-#define RR_EVENT_QSTART 0
-#endif
 #ifndef RR_LD_AUX
 #define RR_LD_AUX 0
 #endif
@@ -77,15 +74,6 @@ namespace {
 // in the end-of-kernel writeback (A/B at N = 65536: 5.49 -> 5.18 us; the same bit on the
 // state planes, which the next launch re-reads, is slower; nt loads +5 %).
 #define RR_OUT_AUX 16
-#endif
-#ifndef RR_STAGGER  // experiment: number of start-delay groups (0 = off)
-#define RR_STAGGER 0
-#endif
-#ifndef RR_STAGGER_BY
-#define RR_STAGGER_BY 0
-#endif
-#ifndef RR_STAGGER_SLEEP
-#define RR_STAGGER_SLEEP 8
 #endif
 #ifndef RR_STEP_ATTR  // occupancy floor of the step kernel: <= 128 VGPRs keeps 4 waves per SIMD at large N
 #define RR_STEP_ATTR __attribute__((amdgpu_waves_per_eu(4)))
@@ -834,20 +822,7 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         const float d2 = 2.0f * c2, d3 = 3.0f * c3;
         const bool pos0 = x0 > 0.0f;
         float lo = 0.0f, hi = 1.0f;  // H(lo) has the sign of x0
-#if RR_EVENT_QSTART
-        // start at the root of the quadratic through x0 (slope hv0) and x1: Q(s) = x0 + hv0 s
-        // + (c2 + c3) s^2, stable form s = x0 / q, q = -(hv0 + sgn(hv0) sqrt(D)) / 2; Q changes
-        // sign on [0, 1], so D > 0 and the root lies in [0, 1]
-        {
-            const float aq = dx - hv0;  // c2 + c3
-            const float D = fmaxf(fmaf(hv0, hv0, -4.0f * aq * x0), 0.0f);
-            const float q = -0.5f * (hv0 + copysignf(fsqrt(D), hv0));
-            s = x0 * frcp(q);
-            s = (s >= 0.0f && s <= 1.0f) ? s : x0 * frcp(x0 - x1);  // (rounding guard: secant)
-        }
-#else
         s = x0 * frcp(x0 - x1);
-#endif
         // Newton from the secant guess, kept inside the closed sign bracket [lo, hi]
         // (bisection fallback). A converged iterate sits on a bracket end, so the test is
         // inclusive. Fixed 3 iterations, branch-free (quadratic convergence from the secant
@@ -1121,12 +1096,6 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     const uint32_t wave_idx = blockIdx.x * WPB + wv;
     const uint32_t wave_base = wave_idx * EPW;
     if (wave_base >= n) return;  // wave-uniform
-#if RR_STAGGER
-    {  // experiment: delay the load burst of some waves (group = wave in block, or block)
-        const uint32_t grp = (RR_STAGGER_BY == 0 ? wv : __builtin_amdgcn_readfirstlane(blockIdx.x / 8u)) % RR_STAGGER;
-        for (uint32_t k = 0; k < grp; ++k) __builtin_amdgcn_s_sleep(RR_STAGGER_SLEEP);
-    }
-#endif
     const uint32_t i = wave_base + lane;
     const bool valid = (EPW == kWave || lane < (uint32_t)EPW) && i < n;
     const uint32_t ic = valid ? i : n - 1;
