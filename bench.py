@@ -50,7 +50,10 @@ def parse():
                          "(fp16x3: operands as fp16 hi + lo, three MFMAs per k step, fp32-level accuracy) or bf16 "
                          "MFMA with fp32 accumulation (opt-in)")
     ap.add_argument("--rollout-two-launch", action="store_true",
-                    help="rollout mode: rr_policy_act + rr_step per step instead of the one-launch rr_rollout_step")
+                    help="rollout mode: rr_policy_act + rr_step per step instead of the one-launch rr_rollout_collect")
+    ap.add_argument("--rollout-per-step", action="store_true",
+                    help="rollout mode: one rr_rollout_step launch per step (+ bootstrap + GAE launches) instead "
+                         "of the whole collect in one rr_rollout_collect launch")
     ap.add_argument("--rollout-torch", action="store_true",
                     help="rollout policy / bootstrap / GAE as PyTorch ops instead of the fused HIP kernels")
     return ap.parse_args()
@@ -72,7 +75,8 @@ def bench_rollout(args, dev, n, model, kw):
     pol = MlpActorCritic(env.state_dim, env.action_dim).to(dev)
     fused = not args.rollout_torch
     ro = DeviceRollout(env, pol, n_steps=args.rollout_steps, fused=fused, policy_dtype=args.policy_dtype,
-                       one_launch=fused and not args.rollout_two_launch and args.integrator != "dopri5")
+                       one_launch=fused and not args.rollout_two_launch and args.integrator != "dopri5",
+                       per_step=args.rollout_per_step)
     for _ in range(3):
         ro.collect()
     torch.cuda.synchronize(dev)
@@ -107,13 +111,16 @@ def bench_rollout(args, dev, n, model, kw):
                   % ("6DOF" if model == 6 else "3DOF", n),
         "value": n * steps / dt, "unit": "env-steps/s", "n_gpus": 1, "steps": steps, "warmup": 3 * args.rollout_steps,
         "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32" if args.policy_dtype == "fp32" else "fp32 env, bf16-MFMA policy towers (fp32 accumulate)",
+        "dtype": {"fp32": "fp32", "fp16x3": "fp32 env, split-fp16 MFMA policy towers (fp16 hi + lo operands, fp32 "
+                  "accumulate)", "bf16": "fp32 env, bf16-MFMA policy towers (fp32 accumulate)"}[args.policy_dtype],
         "data": "synthetic ICs (env_config init_space), actions from a random-init MlpPolicy",
         "config": {"workload": "Rocket6DOF N=%d, MlpPolicy(64x64 tanh) forward + Gaussian sample + fused step "
                                "+ timeout bootstrap + rollout buffer + GAE, n_steps=%d per hipGraph"
                                % (n, args.rollout_steps), "envs_per_gpu": n,
                    "policy_path": "PyTorch ops" if args.rollout_torch else
-                   ("one launch per step: rr_rollout_step (policy on %s MFMA + env step)" if ro.one_launch else
+                   ("one launch per collect: rr_rollout_collect (n_steps x [policy on %s MFMA + env step] + GAE)"
+                    if ro.one_launch and not ro.per_step else
+                    "one launch per step: rr_rollout_step (policy on %s MFMA + env step)" if ro.one_launch else
                     "two launches per step: rr_policy_act (%s MFMA) + rr_step") % args.policy_dtype},
         "gpu_ms_per_collect": e0.elapsed_time(e1) / reps,
         "ppo_epoch_ms": upd * 1e3, "ppo_stats": stats,

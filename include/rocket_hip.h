@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 3
+#define RR_ABI_VERSION 4
 
 /* error codes */
 #define RR_OK 0
@@ -242,6 +242,24 @@ int rr_rollout_step(rr_env* e, const float* params, int precision, uint64_t seed
                     float gamma, float* buf_obs, float* buf_action, float* buf_value, float* buf_log_prob,
                     float* buf_start, float* buf_reward, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
                     float* terms, void* stream);
+
+/* A whole PPO rollout in ONE launch (replaces SB3 OnPolicyAlgorithm.collect_rollouts +
+ * RolloutBuffer.compute_returns_and_advantage, stable_baselines3 1.6 on_policy_algorithm.py /
+ * buffers.py, driving the reference's env through main_6DOF.py:60-120). Steps t = 0..n_steps-1
+ * are exactly rr_rollout_step(t) — same noise key (seed, env id, *iter, t), same env step,
+ * bootstrap and buffer writes, now into the [t] slices of [n_steps][n] buffers — with the env
+ * state kept in registers between steps; then last_value[i] = V(post-step obs) (as
+ * rr_policy_bootstrap), last_done[i] = last_start[i] = float(done[i]) and, when
+ * buf_advantage / buf_return are given, the GAE scan of rr_gae(gamma, gae_lambda). Env outputs
+ * (obs, reward, done, truncated, terms) are those of the last step. last_* / obs / truncated /
+ * terms may be NULL. Bitwise the same results as n_steps rr_rollout_step launches +
+ * rr_policy_bootstrap + rr_gae. RK4 / Euler envs. */
+int rr_rollout_collect(rr_env* e, const float* params, int precision, uint64_t seed, const uint64_t* iter,
+                       int n_steps, float gamma, float gae_lambda, float* buf_obs, float* buf_action,
+                       float* buf_value, float* buf_log_prob, float* buf_start, float* buf_reward,
+                       float* buf_advantage, float* buf_return, float* last_value, float* last_done,
+                       float* last_start, float* obs, float* reward, uint8_t* done, uint8_t* truncated, float* terms,
+                       void* stream);
 
 /* RolloutBuffer.compute_returns_and_advantage: rewards / values / starts [T][n] (starts[t]
  * = episode-start flag of step t), last_value / last_done [n] -> advantages, returns [T][n]. */

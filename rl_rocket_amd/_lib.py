@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
@@ -108,6 +108,8 @@ SIGNATURES = {
                                            ctypes.c_float, _P, _P, _P, _P]),
     "rr_rollout_step": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_uint64, _P, ctypes.c_int, ctypes.c_float,
                                        _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "rr_rollout_collect": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_uint64, _P, ctypes.c_int, ctypes.c_float,
+                                          ctypes.c_float] + [_P] * 17),
     "rr_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, _P,
                               _P, _P]),
 }

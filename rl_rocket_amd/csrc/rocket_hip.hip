@@ -2058,23 +2058,67 @@ int rr_policy_bootstrap(const float* params, int obs_dim, int act_dim, int preci
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_policy_bootstrap: launch");
 }
 
+namespace {
+int launch_rollout(rr_env* e, const char* who, bool multi, const float* params, int precision, uint64_t seed,
+                   const uint64_t* iter, RolloutIO& io, void* stream)
+{
+    if (!params || !iter || !io.buf_obs || !io.buf_act || !io.buf_val || !io.buf_logp || !io.buf_start ||
+        !io.buf_rew || !io.reward || !io.done)
+        return fail(RR_EINVAL, std::string(who) + ": null argument");
+    if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, std::string(who) + ": params must be 16-B aligned");
+    if (precision != RR_POLICY_FP32 && precision != RR_POLICY_BF16 && precision != RR_POLICY_FP16X3)
+        return fail(RR_EINVAL,
+                    std::string(who) + ": precision must be RR_POLICY_FP32, RR_POLICY_BF16 or RR_POLICY_FP16X3");
+    if (e->p.integrator == RR_INT_DOPRI5)
+        return fail(RR_EINVAL, std::string(who) + ": RR_INT_DOPRI5 envs step through rr_policy_act + rr_step");
+    io.params = params;
+    io.iter = iter;
+    io.seed_lo = (uint32_t)seed;
+    io.seed_hi = (uint32_t)(seed >> 32);
+    io.obs_vec_ok = ((uintptr_t)io.obs & 15u) == 0;
+    io.buf_obs_vec_ok = ((uintptr_t)io.buf_obs & 15u) == 0;
+    const Bufs b = bufs_of(e);
+    const uint32_t nn = (uint32_t)e->n;
+    const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
+    const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
+    const dim3 grid((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock)), block(rol::kThreads);
+    hipStream_t s = (hipStream_t)stream;
+    const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
+#define RR_LAUNCH(M, I, PR)                                                                                          \
+    do {                                                                                                             \
+        if (multi)                                                                                                   \
+            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true>), grid, block, 0, s, e->state, nn, mode, e->kp, \
+                               b, io);                                                                               \
+        else                                                                                                         \
+            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, false>), grid, block, 0, s, e->state, nn, mode,      \
+                               e->kp, b, io);                                                                        \
+    } while (0)
+#define RR_LAUNCH_P(M, I)                                           \
+    do {                                                            \
+        if (precision == RR_POLICY_BF16) RR_LAUNCH(M, I, 1);        \
+        else if (precision == RR_POLICY_FP16X3) RR_LAUNCH(M, I, 2); \
+        else RR_LAUNCH(M, I, 0);                                    \
+    } while (0)
+    if (m6 && !euler) RR_LAUNCH_P(6, RR_INT_RK4);
+    else if (m6) RR_LAUNCH_P(6, RR_INT_EULER);
+    else if (!euler) RR_LAUNCH_P(3, RR_INT_RK4);
+    else RR_LAUNCH_P(3, RR_INT_EULER);
+#undef RR_LAUNCH_P
+#undef RR_LAUNCH
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return hip_fail(err, (std::string(who) + ": launch").c_str());
+    e->steps += io.T;
+    return RR_OK;
+}
+}  // namespace
+
 int rr_rollout_step(rr_env* e, const float* params, int precision, uint64_t seed, const uint64_t* iter, int t,
                     float gamma, float* buf_obs, float* buf_action, float* buf_value, float* buf_log_prob,
                     float* buf_start, float* buf_reward, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
                     float* terms, void* stream)
 {
     if (!e) return fail(RR_EINVAL, "rr_rollout_step: null handle");
-    if (!params || !iter || !buf_obs || !buf_action || !buf_value || !buf_log_prob || !buf_start || !buf_reward ||
-        !reward || !done)
-        return fail(RR_EINVAL, "rr_rollout_step: null argument");
-    if (((uintptr_t)params & 15) != 0) return fail(RR_EINVAL, "rr_rollout_step: params must be 16-B aligned");
-    if (precision != RR_POLICY_FP32 && precision != RR_POLICY_BF16 && precision != RR_POLICY_FP16X3)
-        return fail(RR_EINVAL, "rr_rollout_step: precision must be RR_POLICY_FP32, RR_POLICY_BF16 or RR_POLICY_FP16X3");
-    if (e->p.integrator == RR_INT_DOPRI5)
-        return fail(RR_EINVAL, "rr_rollout_step: RR_INT_DOPRI5 envs step through rr_policy_act + rr_step");
-    RolloutIO io;
-    io.params = params;
-    io.iter = iter;
+    RolloutIO io = {};
     io.buf_obs = buf_obs;
     io.buf_act = buf_action;
     io.buf_val = buf_value;
@@ -2086,37 +2130,45 @@ int rr_rollout_step(rr_env* e, const float* params, int precision, uint64_t seed
     io.done = done;
     io.truncated = truncated;
     io.terms = terms;
-    io.seed_lo = (uint32_t)seed;
-    io.seed_hi = (uint32_t)(seed >> 32);
     io.t = (uint32_t)t;
     io.gamma = gamma;
-    io.obs_vec_ok = ((uintptr_t)obs & 15u) == 0;
-    io.buf_obs_vec_ok = ((uintptr_t)buf_obs & 15u) == 0;
-    const Bufs b = bufs_of(e);
-    const uint32_t nn = (uint32_t)e->n;
-    const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
-    const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
-    const dim3 grid((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock)), block(rol::kThreads);
-    hipStream_t s = (hipStream_t)stream;
-    const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
-#define RR_LAUNCH(M, I, PR) \
-    hipLaunchKernelGGL((rollout_step_kernel<M, I, PR>), grid, block, 0, s, e->state, nn, mode, e->kp, b, io)
-#define RR_LAUNCH_P(M, I)                                  \
-    do {                                                   \
-        if (precision == RR_POLICY_BF16) RR_LAUNCH(M, I, 1);     \
-        else if (precision == RR_POLICY_FP16X3) RR_LAUNCH(M, I, 2); \
-        else RR_LAUNCH(M, I, 0);                           \
-    } while (0)
-    if (m6 && !euler) RR_LAUNCH_P(6, RR_INT_RK4);
-    else if (m6) RR_LAUNCH_P(6, RR_INT_EULER);
-    else if (!euler) RR_LAUNCH_P(3, RR_INT_RK4);
-    else RR_LAUNCH_P(3, RR_INT_EULER);
-#undef RR_LAUNCH_P
-#undef RR_LAUNCH
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return hip_fail(err, "rr_rollout_step: launch");
-    e->steps++;
-    return RR_OK;
+    io.T = 1;
+    return launch_rollout(e, "rr_rollout_step", false, params, precision, seed, iter, io, stream);
+}
+
+int rr_rollout_collect(rr_env* e, const float* params, int precision, uint64_t seed, const uint64_t* iter,
+                       int n_steps, float gamma, float gae_lambda, float* buf_obs, float* buf_action,
+                       float* buf_value, float* buf_log_prob, float* buf_start, float* buf_reward,
+                       float* buf_advantage, float* buf_return, float* last_value, float* last_done,
+                       float* last_start, float* obs, float* reward, uint8_t* done, uint8_t* truncated, float* terms,
+                       void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_rollout_collect: null handle");
+    if (n_steps <= 0) return fail(RR_EINVAL, "rr_rollout_collect: n_steps must be positive");
+    if ((buf_advantage == nullptr) != (buf_return == nullptr))
+        return fail(RR_EINVAL, "rr_rollout_collect: buf_advantage and buf_return go together");
+    RolloutIO io = {};
+    io.buf_obs = buf_obs;
+    io.buf_act = buf_action;
+    io.buf_val = buf_value;
+    io.buf_logp = buf_log_prob;
+    io.buf_start = buf_start;
+    io.buf_rew = buf_reward;
+    io.buf_adv = buf_advantage;
+    io.buf_ret = buf_return;
+    io.last_value = last_value;
+    io.last_done = last_done;
+    io.last_start = last_start;
+    io.obs = obs;
+    io.reward = reward;
+    io.done = done;
+    io.truncated = truncated;
+    io.terms = terms;
+    io.t = 0;
+    io.T = (uint32_t)n_steps;
+    io.gamma = gamma;
+    io.lam = gae_lambda;
+    return launch_rollout(e, "rr_rollout_collect", true, params, precision, seed, iter, io, stream);
 }
 
 int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, const float* starts,

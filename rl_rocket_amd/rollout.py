@@ -203,9 +203,11 @@ class DeviceRollout:
     fp32-MFMA HIP launch for policy forward + sampling + buffer writes (``rr_policy_act``),
     the fused env step, one launch for the timeout bootstrap (``rr_policy_bootstrap``);
     GAE in one launch (``rr_gae``). ``fused=False``: the same algorithm in PyTorch ops.
-    ``one_launch=True`` (default where possible: fused, RK4 / Euler env) collapses each step
-    to ONE launch (``rr_rollout_step``: policy, sample, env step, bootstrap and buffer writes
-    in one kernel); bitwise the same rollout as the two-launch sequence.
+    ``one_launch=True`` (default where possible: fused, RK4 / Euler env) collapses the whole
+    ``collect`` to ONE launch (``rr_rollout_collect``: every env runs policy, sample, env step,
+    bootstrap and buffer writes for all ``n_steps`` with its state in registers, then V(last
+    obs) and its GAE scan); ``per_step=True`` keeps one launch per step (``rr_rollout_step``)
+    + bootstrap + GAE launches. All three paths produce bitwise the same rollout.
     ``policy_dtype="fp16x3"`` (fused only) runs the towers on fp16 MFMA with every operand
     split into fp16 hi + lo halves and three MFMAs per k step: fp32-level results (values
     within ~3e-6 of the PyTorch fp32 policy, as the fp32 path) at 1.44x the collection rate.
@@ -215,7 +217,7 @@ class DeviceRollout:
     the bf16 mean; PPO's first-epoch ratio starts within ~1e-3 of 1 instead of at 1)."""
 
     def __init__(self, batch, policy, n_steps=16, gamma=0.99, gae_lambda=0.95, generator=None, fused=None,
-                 seed=0, policy_dtype="fp32", one_launch=None):
+                 seed=0, policy_dtype="fp32", one_launch=None, per_step=False):
         self.env, self.policy = batch, policy
         self.n_steps, self.gamma, self.lam = n_steps, gamma, gae_lambda
         n, ns, na = batch.num_envs, batch.state_dim, batch.action_dim
@@ -251,6 +253,7 @@ class DeviceRollout:
         if one_launch and (not self.fused or dopri):
             raise ValueError("one_launch needs the fused policy and an RK4 / Euler env")
         self.one_launch = bool(one_launch)
+        self.per_step = bool(per_step) or not self.one_launch  # one_launch + not per_step: rr_rollout_collect
         if self.fused:
             from . import _lib
 
@@ -298,8 +301,9 @@ class DeviceRollout:
         self._gae()
 
     def _collect_fused(self):
-        """one_launch: one rr_rollout_step per step (the env's obs buffer is written on the
-        last step only), then V(last obs). Otherwise two launches per step: rr_policy_act
+        """one_launch: the whole rollout + GAE in one rr_rollout_collect launch, or (per_step)
+        one rr_rollout_step per step (the env's obs buffer is written on the last step only),
+        then V(last obs). Otherwise two launches per step: rr_policy_act
         (forward + sample of step t, bootstrap of step t-1, episode-start flags) and the
         fused env step; obs are read in place from the env's output buffer."""
         env, lib, c, p = self.env, self._lib, self._c, self._p
@@ -310,6 +314,15 @@ class DeviceRollout:
         stream = c.c_void_p(torch.cuda.current_stream(env.device).cuda_stream)
         it, obs, done = p(self.iter), p(env.obs), p(env.done)
         prec = self._pack.prec
+        if self.one_launch and not self.per_step:
+            _lib.check(lib.rr_rollout_collect(env._h, params, prec, self.seed, it, self.n_steps, self.gamma, self.lam,
+                                              p(self.obs), p(self.actions), p(self.values), p(self.log_probs),
+                                              p(self.starts), p(self.rewards), p(self.advantages), p(self.returns),
+                                              p(self.last_value), p(self.last_done), p(self.last_start), obs,
+                                              p(env.reward), done, p(env.truncated), p(env.terms), stream),
+                       "rr_rollout_collect")
+            self.iter.add_(1)
+            return
         if self.one_launch:
             T = self.n_steps
             for t in range(T):

@@ -247,10 +247,11 @@ def test_fused_collect_matches_semantics(fused, prec):
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16x3"])
 @pytest.mark.parametrize("model", [6, 3])
 def test_one_launch_rollout_bitwise_equals_two_launch(model, prec):
-    """rr_rollout_step (policy + env step in one kernel) against rr_policy_act + rr_step:
-    every rollout buffer, the env outputs and the env state bitwise equal over two collects
-    (TimeLimit 6 < n_steps: truncation bootstraps and auto-resets inside the rollout; ragged
-    N: idle waves in the last workgroup)."""
+    """rr_rollout_collect (the whole rollout + GAE in one kernel) and rr_rollout_step (policy +
+    env step in one kernel per step) against rr_policy_act + rr_step: every rollout buffer,
+    the env outputs (incl. reward terms), the terminal rows and the env state bitwise equal
+    over two collects (TimeLimit 6 < n_steps: truncation bootstraps and auto-resets inside the
+    rollout; ragged N: idle waves in the last workgroup)."""
     import torch
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
@@ -261,25 +262,29 @@ def test_one_launch_rollout_bitwise_equals_two_launch(model, prec):
     kw = ENV_CONFIG_6DOF if model == 6 else {}
     pol = _policy(ns, na, seed=3)
     ros = []
-    for one in (False, True):
-        env = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=6, **kw)
-        ro = DeviceRollout(env, pol, n_steps=T, policy_dtype=prec, one_launch=one, seed=11)
-        assert ro.one_launch == one
+    for one, per_step in ((False, True), (True, True), (True, False)):
+        env = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=6, compute_terms=True, **kw)
+        ro = DeviceRollout(env, pol, n_steps=T, policy_dtype=prec, one_launch=one, per_step=per_step, seed=11)
+        assert ro.one_launch == one and ro.per_step == per_step
         ros.append(ro)
     for _ in range(2):
         for ro in ros:
             ro.collect()
         torch.cuda.synchronize()
-        a, b = ros
-        for name in ("obs", "actions", "values", "log_probs", "starts", "rewards", "advantages", "returns",
-                     "last_value", "last_done"):
-            x, y = getattr(a, name), getattr(b, name)
-            assert torch.equal(x, y), (name, (x - y).abs().max().item())
-        for name in ("obs", "reward", "done", "truncated"):
-            assert torch.equal(getattr(a.env, name), getattr(b.env, name)), name
-        sa, sb = a.env.get_state(), b.env.get_state()
-        for x, y in zip(sa, sb):
-            assert torch.equal(x, y)
+        a = ros[0]
+        for b in ros[1:]:
+            for name in ("obs", "actions", "values", "log_probs", "starts", "rewards", "advantages", "returns",
+                         "last_value", "last_done", "last_start"):
+                x, y = getattr(a, name), getattr(b, name)
+                assert torch.equal(x, y), (name, b.per_step, (x - y).abs().max().item())
+            for name in ("obs", "reward", "done", "truncated", "terms"):
+                assert torch.equal(getattr(a.env, name), getattr(b.env, name)), (name, b.per_step)
+            for x, y in zip(a.env.get_state(), b.env.get_state()):
+                assert torch.equal(x, y), b.per_step
+            ta, tb = a.env.copy_terminal(), b.env.copy_terminal()
+            for x, y in zip(ta, tb):
+                assert torch.equal(x, y), b.per_step
+            assert torch.equal(a.iter, b.iter)
     assert a.starts[1:].sum() > 0 and (a.rewards != 0).any()
     for ro in ros:
         ro.env.close()
