@@ -2081,17 +2081,25 @@ int launch_rollout(rr_env* e, const char* who, bool multi, const float* params, 
     const uint32_t nn = (uint32_t)e->n;
     const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
     const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
-    const dim3 grid((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock)), block(rol::kThreads);
+    const dim3 grid((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock));
+    // rr_rollout_collect: 64 envs per wave; RR_ROLLOUT_NT=1 selects 32 envs per wave (two waves
+    // per SIMD; measured 2-16 % slower at N = 65536: the env step's VALU work doubles). Read per
+    // call, so tests cover both shapes in one process.
+    const char* ntv = std::getenv("RR_ROLLOUT_NT");
+    const int ntw = (multi && ntv && std::atoi(ntv) == 1) ? 1 : 2;
     hipStream_t s = (hipStream_t)stream;
     const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
-#define RR_LAUNCH(M, I, PR)                                                                                          \
-    do {                                                                                                             \
-        if (multi)                                                                                                   \
-            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true>), grid, block, 0, s, e->state, nn, mode, e->kp, \
-                               b, io);                                                                               \
-        else                                                                                                         \
-            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, false>), grid, block, 0, s, e->state, nn, mode,      \
-                               e->kp, b, io);                                                                        \
+#define RR_LAUNCH(M, I, PR)                                                                                        \
+    do {                                                                                                           \
+        if (!multi)                                                                                                \
+            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, false, 2>), grid, dim3(rol::Shape<2>::kThreads), 0, \
+                               s, e->state, nn, mode, e->kp, b, io);                                               \
+        else if (ntw == 2)                                                                                         \
+            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true, 2>), grid, dim3(rol::Shape<2>::kThreads), 0,  \
+                               s, e->state, nn, mode, e->kp, b, io);                                               \
+        else                                                                                                       \
+            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true, 1>), grid, dim3(rol::Shape<1>::kThreads), 0,  \
+                               s, e->state, nn, mode, e->kp, b, io);                                               \
     } while (0)
 #define RR_LAUNCH_P(M, I)                                           \
     do {                                                            \
