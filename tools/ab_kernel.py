@@ -35,6 +35,9 @@ def main():
     libs = []
     for k, spec in enumerate(a.sources):
         src, _, defs = spec.partition("@")  # "file.hip@NAME=VAL,NAME2=VAL2"
+        if src.endswith(".so"):  # prebuilt variant (compiled on the CPU side)
+            libs.append(os.path.abspath(src))
+            continue
         lib = os.path.join(a.out, "ab_%d.so" % k)
         items = [d for d in defs.split(",") if d]  # "+flag" items are extra compiler flags
         cmd = b.command(out=lib, defines=tuple(d for d in items if not d.startswith("+")),
