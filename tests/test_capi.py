@@ -51,6 +51,11 @@ def test_invalid_arguments_fail_cleanly_without_gpu():
     assert lib.rr_step(None, None, None, None, None, None, None, None) == _lib.RR_EINVAL
     assert lib.rr_destroy(None) == 0
     assert lib.rr_num_envs(None) == -1
+    # rollout entry points: argument errors come back as codes before any HIP call
+    assert lib.rr_rollout_step(None, None, 0, 0, None, 0, 0.99, *([None] * 12)) == _lib.RR_EINVAL
+    assert lib.rr_rollout_collect(None, None, 0, 0, None, 16, 0.99, 0.95, *([None] * 17)) == _lib.RR_EINVAL
+    assert b"rr_rollout_collect" in lib.rr_last_error()
+    assert lib.rr_gae(0, 16, None, None, None, None, None, 0.99, 0.95, None, None, None) == _lib.RR_EINVAL
 
 
 def _c_layout(struct, fields):
