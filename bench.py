@@ -61,7 +61,7 @@ def parse():
     return ap.parse_args()
 
 
-def bench_rollout(args, dev, n, model, kw):
+def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
     """BASELINE configs[4]: N envs driving an on-device PPO rollout; the whole collect()
     (n_steps x [policy forward, Gaussian sample, env step, timeout bootstrap, buffer
     writes] + GAE) is one hipGraph; obs never leave HBM."""
@@ -73,7 +73,7 @@ def bench_rollout(args, dev, n, model, kw):
 
     torch.manual_seed(42)
     env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
-                      episode_stats=False, integrator=args.integrator, **kw)
+                      episode_stats=False, integrator=args.integrator, env_id_offset=rank * n, **kw)
     pol = MlpActorCritic(env.state_dim, env.action_dim).to(dev)
     fused = not args.rollout_torch
     ro = DeviceRollout(env, pol, n_steps=args.rollout_steps, fused=fused, policy_dtype=args.policy_dtype,
@@ -93,6 +93,9 @@ def bench_rollout(args, dev, n, model, kw):
     torch.cuda.synchronize(dev)
     reps = max(2, args.steps // args.rollout_steps)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     e0.record()
     for _ in range(reps):
@@ -100,18 +103,23 @@ def bench_rollout(args, dev, n, model, kw):
     e1.record()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    if dist is not None:  # max over ranks of the timed region
+        t = torch.tensor([dt], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
     steps = reps * args.rollout_steps
     opt = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    stats = ppo_update(pol, opt, ro, n_epochs=1, batch_size=n)
+    # one policy replica per GPU: minibatch gradients averaged over the ranks (one all_reduce)
+    stats = ppo_update(pol, opt, ro, n_epochs=1, batch_size=n, group=dist.group.WORLD if dist is not None else None)
     torch.cuda.synchronize(dev)
     upd = time.perf_counter() - t1
     env.close()
     return {
         "metric": "env-steps/sec of on-device PPO rollout collection (%s, N=%d per GPU)"
                   % ("6DOF" if model == 6 else "3DOF", n),
-        "value": n * steps / dt, "unit": "env-steps/s", "n_gpus": 1, "steps": steps, "warmup": 3 * args.rollout_steps,
+        "value": n * world * steps / dt, "unit": "env-steps/s", "n_gpus": world, "steps": steps, "warmup": 3 * args.rollout_steps,
         "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": {"fp32": "fp32", "fp16x3": "fp32 env, split-fp16 MFMA policy towers (fp16 hi + lo operands, fp32 "
                   "accumulate)", "bf16": "fp32 env, bf16-MFMA policy towers (fp32 accumulate)"}[args.policy_dtype],
@@ -235,7 +243,7 @@ def main():
     kw = ENV_CONFIG_6DOF if model == 6 else {}
     n = args.n
     if args.mode == "rollout":
-        res = bench_rollout(args, dev, n, model, kw)
+        res = bench_rollout(args, dev, n, model, kw, dist=dist, rank=rank, world=world)
         if rank == 0:
             print(json.dumps(res), flush=True)
         if dist is not None:

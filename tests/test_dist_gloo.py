@@ -65,3 +65,81 @@ def test_gather_world2_gloo():
         np.testing.assert_array_equal(o[:, 0], gid)
         np.testing.assert_array_equal(r, -gid)
         np.testing.assert_array_equal(d, (gid.astype(int) % 3 == 0).astype(np.uint8))
+
+
+class _FakeRollout:
+    """The fields ppo_update reads from a DeviceRollout, on the host."""
+
+    def __init__(self, seed, n_steps=4, n_envs=32, ns=14, na=3):
+        g = torch.Generator().manual_seed(seed)
+
+        class _Env:
+            num_envs = n_envs
+
+        self.env, self.n_steps = _Env(), n_steps
+        self.obs = torch.randn((n_steps, n_envs, ns), generator=g)
+        self.actions = torch.randn((n_steps, n_envs, na), generator=g)
+        self.log_probs = torch.randn((n_steps, n_envs), generator=g) - 3.0
+        self.advantages = torch.randn((n_steps, n_envs), generator=g)
+        self.returns = torch.randn((n_steps, n_envs), generator=g)
+
+
+def _ppo_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rl_rocket_amd.rollout import MlpActorCritic, ppo_update
+
+    torch.manual_seed(0)  # replicas start equal
+    pol = MlpActorCritic(14, 3)
+    opt = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5)
+    ro = _FakeRollout(seed=100 + rank)  # each rank's own env shard
+    ppo_update(pol, opt, ro, n_epochs=1, batch_size=ro.n_steps * ro.env.num_envs, group=dist.group.WORLD)
+    q.put((rank, [p.detach().numpy().copy() for p in pol.parameters()]))  # numpy: no shared-memory handles
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ppo_replicas_allreduce_world2_gloo():
+    """One policy replica per rank: after an update on different local
+    rollouts the replicas are identical, and equal to one optimizer step on the average of
+    the two ranks' gradients."""
+    from rl_rocket_amd.rollout import MlpActorCritic
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ppo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)
+    # reference: the same minibatch loss on each rank's data, gradients averaged, one step
+    torch.manual_seed(0)
+    ref = MlpActorCritic(14, 3)
+    grads = []
+    for rank in range(world):
+        ro = _FakeRollout(seed=100 + rank)
+        n = ro.n_steps * ro.env.num_envs
+        ref.zero_grad(set_to_none=True)
+        mean, value = ref(ro.obs.reshape(n, -1))
+        lp = ref.log_prob(mean, ro.actions.reshape(n, -1))
+        adv = ro.advantages.reshape(n)
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        ratio = torch.exp(lp - ro.log_probs.reshape(n))
+        pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 0.8, 1.2)).mean()
+        vf = torch.nn.functional.mse_loss(ro.returns.reshape(n), value)
+        loss = pg + 0.01 * (-ref.entropy(n).mean()) + 0.5 * vf
+        loss.backward()
+        grads.append([p.grad.clone() for p in ref.parameters()])
+    for p, g0, g1 in zip(ref.parameters(), *grads):
+        p.grad = (g0 + g1) / 2
+    torch.nn.utils.clip_grad_norm_(ref.parameters(), 0.5)
+    torch.optim.Adam(ref.parameters(), lr=3e-4, eps=1e-5).step()
+    for a, b in zip(res[0], ref.parameters()):
+        np.testing.assert_allclose(a, b.detach().numpy(), atol=1e-6, rtol=1e-5)
