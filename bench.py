@@ -270,24 +270,31 @@ def main():
         one(k)
     torch.cuda.synchronize(dev)
 
-    # ---- timed region: K steps (hipGraph replays of graph_steps launches each) ----
+    # ---- timed region: exactly K steps (hipGraph replays) ----
     use_graph = not args.no_graph and not args.allgather
-    gs = args.graph_steps
-    if use_graph:
-        graph = torch.cuda.CUDAGraph()
+    # exactly K steps: K // gs replays of a gs-launch graph (gs balanced so that K = 2000 is
+    # 2 x 1000, not 1024 + 976) plus one graph of the K % gs remainder launches
+    K = args.steps
+    gs = max(1, -(-K // max(1, -(-K // max(1, args.graph_steps)))))
+    rem = K % gs
+
+    def capture(n_launch):
+        g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(dev)
         s.wait_stream(stream)
         with torch.cuda.stream(s):
-            with torch.cuda.graph(graph, stream=s):
-                for k in range(gs):
+            with torch.cuda.graph(g, stream=s):
+                for k in range(n_launch):
                     env.step(pool[k % POOL])
         stream.wait_stream(s)
         torch.cuda.synchronize(dev)
-        graph.replay()  # warm the graph
+        g.replay()  # warm the graph
         torch.cuda.synchronize(dev)
-    K = args.steps
+        return g
+
     if use_graph:
-        K = max(gs, (K + gs - 1) // gs * gs)
+        graph = capture(gs)
+        graph_rem = capture(rem) if rem else None
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -297,6 +304,8 @@ def main():
     if use_graph:
         for _ in range(K // gs):
             graph.replay()
+        if graph_rem is not None:
+            graph_rem.replay()
     else:
         for k in range(K):
             one(k)
