@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--integrator", default="rk4")
     ap.add_argument("--allgather", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--launch", default="graph", choices=["graph", "loop"],
+                    help="graph: K launches replayed from hipGraphs; loop: one rr_step_repeat call (K launches "
+                         "issued back to back from C, action batch t % 8 of the resident pool)")
     ap.add_argument("--graph-steps", type=int, default=1024,
                     help="env steps captured per hipGraph (each replay costs a fixed ~15-20 us on the GPU "
                          "timeline: 64 -> 4.34 us/step, 256 -> 4.25, 1024 -> 4.18 at N=65536)")
@@ -271,7 +274,8 @@ def main():
     torch.cuda.synchronize(dev)
 
     # ---- timed region: exactly K steps (hipGraph replays) ----
-    use_graph = not args.no_graph and not args.allgather
+    use_graph = not args.no_graph and not args.allgather and args.launch == "graph"
+    use_loop = args.launch == "loop" and not args.allgather
     # exactly K steps: K // gs replays of a gs-launch graph (gs balanced so that K = 2000 is
     # 2 x 1000, not 1024 + 976) plus one graph of the K % gs remainder launches
     K = args.steps
@@ -295,6 +299,10 @@ def main():
     if use_graph:
         graph = capture(gs)
         graph_rem = capture(rem) if rem else None
+    # Device time of the K launches: HIP events on the launch stream around the replays. It
+    # includes hipGraphLaunch's fixed preamble on the GPU timeline (~6-8 us per replay, so
+    # +0.3-0.4 us per step at the driver's K = 20); event-record nodes inside the graph, which
+    # would exclude it, are refused by torch on ROCm ("External events are disallowed").
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -306,6 +314,8 @@ def main():
             graph.replay()
         if graph_rem is not None:
             graph_rem.replay()
+    elif use_loop:
+        env.step_repeat(pool, K)
     else:
         for k in range(K):
             one(k)
@@ -345,13 +355,16 @@ def main():
                                   "RCCL all_gather of obs/reward/done each step" if args.allgather else
                                   "no data-path collective"),
                    "envs_per_gpu": n, "global_envs": n * world, "integrator": args.integrator,
-                   "graph_steps": gs if use_graph else 0,
+                   "graph_steps": gs if use_graph else 0, "launch": "graph" if use_graph else
+                   ("rr_step_repeat" if use_loop else "rr_step per step"),
                    "parallelism": "env-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "B/launch",
                      "traffic_source": traffic_src,
                      "kernel": "step_kernel<%d,%s>" % (model, args.integrator.upper()),
-                     "kernel_us": kern_ms * 1e3, "bytes_per_launch": bytes_launch,
+                     "kernel_us": kern_ms * 1e3,
+                     "timing": "HIP events on the launch stream around the K launches of the timed region",
+                     "bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": BYTES_PER_STEP[model]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

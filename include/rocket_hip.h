@@ -149,6 +149,14 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream);
 int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
             float* terms, void* stream);
 
+/* n_steps consecutive rr_step launches on `stream`, step t taking action batch t % n_batches
+ * of `actions` ([n_batches][N][action_dim], or [n_batches][action_dim][N] planes with
+ * RR_FLAG_ACTION_SOA) — open-loop action sequences already resident on the device (e.g. a
+ * benchmark or a replayed plan) without one host call per step. Outputs as rr_step, of the
+ * last step. */
+int rr_step_repeat(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs, float* reward,
+                   uint8_t* done, uint8_t* truncated, float* terms, void* stream);
+
 /* Overwrite / read the per-env state (parity injection, checkpoint / restore).
  * state_soa [state_dim][N] fp32; v0 [N] or NULL (kept on set / skipped on get);
  * elapsed [N] or NULL (zeroed on set / skipped on get) is the per-env counter word:

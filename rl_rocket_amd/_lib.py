@@ -92,6 +92,7 @@ SIGNATURES = {
     "rr_seed": (ctypes.c_int, [_P, ctypes.c_uint64, _P]),
     "rr_reset": (ctypes.c_int, [_P, _P, _P, _P]),
     "rr_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "rr_step_repeat": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, _P]),
     "rr_set_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_get_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_set_state64": (ctypes.c_int, [_P, _P, _P, _P, _P]),
@@ -134,6 +135,8 @@ def load(require_torch=True):
             "`python -m rl_rocket_amd.build` (hipcc, gfx950). There is no CPU fallback." % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("RR_LIB_PATH") and not hasattr(lib, name):
+            continue  # an older diagnostic build (tools/ab_kernel.py) may lack newer entry points
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

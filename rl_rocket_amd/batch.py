@@ -95,6 +95,21 @@ class RocketBatch:
                                     _ptr(self.truncated), _ptr(self.terms), self._stream()), "rr_step")
         return self.obs, self.reward, self.done, self.truncated
 
+    def step_repeat(self, actions, n_steps):
+        """`n_steps` consecutive steps, step t taking action batch t % len(actions) of the device
+        tensor `actions` [B][N][action_dim] (rr_step_repeat: one host call). Returns the output
+        tensors of the last step."""
+        t = self.torch
+        if not isinstance(actions, t.Tensor) or actions.device != self.device or actions.dtype != t.float32:
+            raise TypeError("actions must be a float32 tensor on %s" % self.device)
+        shape = (self.action_dim, self.num_envs) if self.action_soa else (self.num_envs, self.action_dim)
+        actions = actions.reshape((-1,) + shape).contiguous()
+        self._last_action = actions
+        _lib.check(self.lib.rr_step_repeat(self._h, _ptr(actions), actions.shape[0], int(n_steps), _ptr(self.obs),
+                                           _ptr(self.reward), _ptr(self.done), _ptr(self.truncated), _ptr(self.terms),
+                                           self._stream()), "rr_step_repeat")
+        return self.obs, self.reward, self.done, self.truncated
+
     def set_state(self, state_soa, v0=None, elapsed=None):
         t = self.torch
         st = t.as_tensor(state_soa, device=self.device, dtype=t.float32).reshape(self.state_dim, self.num_envs)

@@ -29,19 +29,6 @@
 
 #include "rocket_hip.h"
 
-// Diagnostic ablations (tools/diag_kernel.py only; the product build has RR_DIAG 0):
-//   1 = memory only (no integration / reward arithmetic), 2 = no event / reset branches,
-//   3 = compute only (state synthesised in registers instead of loaded),
-//   4 = product kernel + s_memtime phase stamps per wave (rr_debug_stamps),
-//   5 = no event path, 6 = no in-kernel reset, 7 = empty kernel (launch + dispatch floor),
-//   8 = empty kernel allocating RR_DIAG8_V + 1 VGPRs, 9 = reward terms skipped (bounds kept),
-//   10 = v0 not loaded, 11 = action not loaded (timing probes).
-#ifndef RR_DIAG
-#define RR_DIAG 0
-#endif
-// per-wave stamp buffer (rr_debug_stamps): 4 = phase stamps, 12 = start / end only (no waits
-// inside the wave, so the wave runs the product code; records its event / done lane counts)
-#define RR_STAMPS (RR_DIAG == 4 || RR_DIAG == 12)
 
 namespace {
 
@@ -56,9 +43,6 @@ namespace {
 #endif
 #ifndef RR_OBS_PACKED
 #define RR_OBS_PACKED 1
-#endif
-#ifndef RR_EARLY_RESET  // 1 = draw the auto-reset candidate during the load wait
-#define RR_EARLY_RESET 1
 #endif
 #ifndef RR_NEWTON_ITERS
 #define RR_NEWTON_ITERS 3
@@ -151,7 +135,7 @@ struct KParams {
 // kernel arguments once at kernel start and pinned (pin_s) so the compiler cannot
 // rematerialise them as scalar loads later: a lone wave per SIMD would otherwise stall
 // on ~20 dependent s_load/s_waitcnt round trips inside the reward code (measured with
-// the RR_DIAG=4 stamps: 2380 cycles for ~150 instructions).
+// per-wave s_memtime stamps in round 1: 2380 cycles for ~150 instructions).
 struct HotParams {
     float inv_norm[RR_MAX_STATE];
     float blo[3], bhi[3];
@@ -212,9 +196,6 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
 }
 
 struct Bufs {
-#if RR_STAMPS
-    uint64_t* stamps;         // [waves][12]: 8 s_memtime phase stamps, s_memrealtime at start / end, XCC_ID, HW_ID
-#endif
     float* state;
     float* v0;
     uint32_t* counter;        // [N] elapsed | episode << 16
@@ -247,20 +228,6 @@ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elemen
 __device__ __forceinline__ f2 pk_his(f2 a, f2 b) { return __builtin_shufflevector(a, b, 1, 3); }  // (a.hi, b.hi)
 __device__ __forceinline__ f2 pk_bc(float x) { return f2{x, x}; }
 
-#if RR_DIAG == 4
-#define RR_STAMP(k)                                                                     \
-    do {                                                                                \
-        uint64_t t_;                                                                    \
-        __builtin_amdgcn_sched_barrier(0);                                              \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");    \
-        __builtin_amdgcn_sched_barrier(0);                                              \
-        stamp_[k] = t_;                                                                 \
-    } while (0)
-#else
-#define RR_STAMP(k) \
-    do {            \
-    } while (0)
-#endif
 
 // Raw buffer access (SRSRC descriptor built from wave-uniform values): 32-bit per-lane
 // voffset, per-plane offsets in soffset (SGPR) — no per-lane 64-bit address arithmetic.
@@ -906,8 +873,12 @@ __device__ __forceinline__ void sample_ic(const KParams& P, ResetStream& k, floa
 
 // Bounds violation on the float32 post-step state: 6DOF Box(lo, hi, float32).contains(r)
 // (rocket_env.py:1036-1038, inclusive); 3DOF _check_bounds (rocket_env.py:431-447).
-template <int MODEL>
-__device__ __forceinline__ bool bounds_hit(const HotParams& P, const float* s)
+struct BoxParams {
+    float blo[3], bhi[3];
+};
+
+template <int MODEL, class BP>
+__device__ __forceinline__ bool bounds_hit(const BP& P, const float* s)
 {
     if constexpr (MODEL == 6) {
         const bool inside = (s[0] >= P.blo[0]) & (s[0] <= P.bhi[0]) & (s[1] >= P.blo[1]) & (s[1] <= P.bhi[1]) &
@@ -1031,42 +1002,129 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
     }
 }
 
-// One launch = one env step of all N envs. Every HBM access goes through a buffer
-// descriptor: the per-lane byte offset is one 32-bit VGPR (i*4), plane offsets are
-// wave-uniform soffsets (NS*N*4 < 4 GiB, checked at rr_create).
-// EPW = envs per wave (one env per lane). 32 envs per wave (half-empty waves, two per
-// SIMD at N = 65536) was measured slower at every N (tools/diag_kernel.py).
-// The leading four arguments are plain pointers / words so that the command processor
-// preloads them into user SGPRs at wave launch (-mllvm -amdgpu-kernarg-preload-count,
-// rl_rocket_amd/build.py): the first state loads then issue without waiting for scalar
-// loads of the kernarg segment. `mode` = rr_params.flags | kModeCounter.
-// ASOA: action layout [NA][N] (RR_FLAG_ACTION_SOA) as a template parameter: a runtime
-// branch between the two layouts made the waitcnt pass stall the wave on the state loads
-// before it issued the action load (two serial memory round trips).
-template <int MODEL, int INTEG, bool ASOA, bool HELP = false, int WPB = kWavesPerBlock, int EPW = kWave>
+// ---------------------------------------------------------------------------
+// Step kernels. One launch = one env step of all N envs. Every HBM access goes through a
+// buffer descriptor: the per-lane byte offset is one 32-bit VGPR (i*4), plane offsets are
+// wave-uniform soffsets (NS*N*4 < 4 GiB, checked at rr_create). The leading four arguments
+// are plain pointers / words so that the command processor preloads them into user SGPRs at
+// wave launch (-mllvm -amdgpu-kernarg-preload-count, rl_rocket_amd/build.py): the first
+// state loads then issue without waiting for scalar loads of the kernarg segment.
+// `mode` = rr_params.flags | kModeCounter. ASOA: action layout [NA][N] (RR_FLAG_ACTION_SOA)
+// as a template parameter (a runtime branch between the two layouts made the waitcnt pass
+// stall the wave on the state loads before it issued the action load).
+// ---------------------------------------------------------------------------
+
+// the action row of env `vo / 4` ([N][NA] rows or [NA][N] planes)
+template <int NA, bool ASOA>
+__device__ __forceinline__ void load_action(rsrc_t act_r, uint32_t vo, uint32_t plane, float* a)
+{
+    if constexpr (ASOA) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
+    } else if constexpr (NA == 3) {
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)((vo << 1) + vo), 0, RR_LD_AUX);  // 12 B rows
+        a[0] = __uint_as_float(v.x);
+        a[1] = __uint_as_float(v.y);
+        a[2] = __uint_as_float(v.z);
+    } else {
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(vo << 1), 0, RR_LD_AUX);  // 8 B rows
+        a[0] = __uint_as_float(v.x);
+        a[1] = __uint_as_float(v.y);
+    }
+}
+
+// Simulator*.step (simulator.py:227-257 / :55-80): integrator, terminal ground event,
+// quaternion renormalisation / theta wrap. Returns the event flag (solve_ivp status 1).
+template <int MODEL, int INTEG>
+__device__ __forceinline__ bool physics_step(const KParams& P, const float* a, const float* y0, float* y1)
+{
+    constexpr int NS = Dims<MODEL>::NS, EV = Dims<MODEL>::EV;
+    float f0[NS];
+    const Ctl c = make_ctl<MODEL>(P, a);
+    integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
+    const float g0 = y0[EV], g1 = y1[EV];
+    const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
+    if (event) event_step<MODEL>(P, c, y0, f0, y1);
+    post_integrate<MODEL>(y1);
+    return event;
+}
+
+// gym TimeLimit (main_6DOF.py:21): elapsed += 1; at the limit done = True and
+// info["TimeLimit.truncated"] = not done. Returns the new elapsed count.
+__device__ __forceinline__ int32_t time_limit(const KParams& P, uint32_t cw, bool& done, bool& trunc)
+{
+    const int32_t el = (int32_t)(cw & kElapsedMask) + 1;
+    trunc = false;
+    if (P.max_steps > 0 && el >= P.max_steps) {
+        trunc = !done;
+        done = true;
+    }
+    return el;
+}
+
+// terminal obs / return / length of a done env (info["terminal_observation"], Monitor):
+// row i of [N][NS] as 16-B stores (rows are 4-B aligned; gfx950 buffer stores need only
+// dword alignment), NS = 14 -> 3 x 16 B + 8 B, NS = 7 -> 16 B + 12 B
+template <int NS>
+__device__ __forceinline__ void store_terminal(const Bufs& B, uint32_t i, uint32_t vo, uint32_t plane, const float* o,
+                                               float ret, int32_t el)
+{
+    const rsrc_t tr = make_rsrc(B.term_obs, (uint64_t)NS * plane);
+    const uint32_t ro = NS == 14 ? (i << 6) - (i << 3) : i * (NS * 4u);  // i * 56 without v_mul_lo_u32
+    auto u4 = [&](int j) {
+        return u32x4{__float_as_uint(o[j]), __float_as_uint(o[j + 1]), __float_as_uint(o[j + 2]),
+                     __float_as_uint(o[j + 3])};
+    };
+#pragma unroll
+    for (int j = 0; j + 4 <= NS; j += 4) __builtin_amdgcn_raw_buffer_store_b128(u4(j), tr, (int)(ro + j * 4), 0, 0);
+    if constexpr (NS % 4 == 2)
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
+                                              (int)(ro + (NS - 2) * 4), 0, 0);
+    else if constexpr (NS % 4 == 3)
+        __builtin_amdgcn_raw_buffer_store_b96(
+            u32x3{__float_as_uint(o[NS - 3]), __float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
+            (int)(ro + (NS - 3) * 4), 0, 0);
+    bst_f<0>(make_rsrc(B.term_ret, plane), ret, vo, 0);
+    bst_u<0>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
+}
+
+// per-env step outputs owned by the caller: reward, done, truncated, optional terms
+template <int NT>
+__device__ __forceinline__ void store_outputs(const StepIO& io, uint32_t i, uint32_t vo, uint32_t plane, uint32_t n,
+                                              float r, bool done, bool trunc, const float* t, bool bv, bool event)
+{
+    bst_f<RR_OUT_AUX>(make_rsrc(io.reward, plane), r, vo, 0);
+    bst_u8<RR_OUT_AUX>(make_rsrc(io.done, n), (uint8_t)done, i);
+    if (io.truncated) bst_u8<RR_OUT_AUX>(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
+    if (io.terms) {
+        const rsrc_t tr = make_rsrc(io.terms, (uint64_t)(NT + 2) * plane);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bst_f(tr, t[j], vo, j * plane);
+        bst_f(tr, bv ? 1.0f : 0.0f, vo, NT * plane);           // info["bounds_violation"]
+        bst_f(tr, event ? 1.0f : 0.0f, vo, (NT + 1) * plane);  // solve_ivp status == 1
+    }
+}
+
+// The step kernel: one env per lane, 64 envs per wave.
+// HELP (N <= RR_HELP_MAX_N, about one main wave per SIMD): the auto-reset candidates of main
+// wave k are drawn by helper wave WPB + k of the same workgroup (on the same SIMD) into
+// cand[k] (row per lane: NS values, v0), published by cflag[k]. A lone wave issues one VALU op
+// per 4 cycles and its SIMD can take one per 2 (MI355X_MICROARCH.md, 'vector-instruction ISSUE
+// cost'), so the helper's ~190 instructions run beside the main wave's instead of before them
+// (they need the counter word, which arrives with the state planes). Without HELP the main
+// wave draws the candidate itself right after its counter word lands. Measured and rejected
+// (round 2): a helper that also computes reward, obs and every caller-owned output while the
+// main wave resets and stores the state (bitwise equal, 4.69 vs 4.31 us per step at N = 65536).
+template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB = kWavesPerBlock>
 __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR void step_kernel(
     float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
     const Bufs B, const StepIO io)
 {
-    constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
-    __shared__ __attribute__((aligned(16))) float lds[WPB][EPW * NS];
-    // HELP: the auto-reset candidates of main wave k are drawn by helper wave k + 4 of the
-    // same workgroup (on the same SIMD) into cand[k] (row per lane: NS values, v0, pad),
-    // published by cflag[k]. A lone wave issues one VALU op per 4 cycles and its SIMD can
-    // take one per 2, so the helper's ~190 instructions run beside the main wave's instead
-    // of before them (they need the counter word, which arrives with the state planes).
+    constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT;
+    __shared__ __attribute__((aligned(16))) float lds[WPB][kWave * NS];
     constexpr int kCandRow = (NS + 1 + 3) / 4 * 4;
     __shared__ __attribute__((aligned(16))) float cand[HELP ? WPB : 1][HELP ? kWave * kCandRow : 1];
     __shared__ uint32_t cflag[WPB];
-#if RR_DIAG == 7
-    return;  // launch + dispatch floor
-#endif
-#if RR_DIAG == 8  // empty kernel that allocates RR_DIAG8_V + 1 VGPRs: dispatch cost vs VGPR count
-#define RR_STR2(x) #x
-#define RR_STR(x) RR_STR2(x)
-    asm volatile("s_nop 0" ::: "v" RR_STR(RR_DIAG8_V));
-    return;
-#endif
     const uint32_t lane = threadIdx.x & (kWave - 1);
     // wave index as an SGPR: derived from threadIdx it is a VGPR the compiler cannot prove
     // uniform, and every buffer store with a wave_base soffset became a waterfall loop
@@ -1077,7 +1135,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
         __syncthreads();  // flags cleared before any helper can publish
         if (wv >= (uint32_t)WPB) {
             const uint32_t k = wv - WPB;  // the main wave this helper serves
-            const uint32_t base = (blockIdx.x * WPB + k) * EPW;
+            const uint32_t base = (blockIdx.x * WPB + k) * kWave;
             if ((mode & RR_FLAG_AUTO_RESET) && base < n) {
                 const uint32_t ih = min(base + lane, n - 1);
                 const uint32_t cwh = (mode & kModeCounter) ? at(B.counter, ih) : 0u;
@@ -1094,10 +1152,10 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
         }
     }
     const uint32_t wave_idx = blockIdx.x * WPB + wv;
-    const uint32_t wave_base = wave_idx * EPW;
+    const uint32_t wave_base = wave_idx * kWave;
     if (wave_base >= n) return;  // wave-uniform
     const uint32_t i = wave_base + lane;
-    const bool valid = (EPW == kWave || lane < (uint32_t)EPW) && i < n;
+    const bool valid = i < n;
     const uint32_t ic = valid ? i : n - 1;
     const uint32_t vo = ic * 4u;           // per-lane byte offset in every fp32/u32 plane
     const uint32_t plane = n * 4u;         // bytes per plane
@@ -1105,50 +1163,18 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     // state planes, v0, counter and ep_ret are consecutive planes of ONE allocation
     // (rr_create), so a single descriptor (4 SGPRs) serves them all via soffset
     const rsrc_t st_r = make_rsrc(state, (uint64_t)(NS + 3) * plane);
-    const rsrc_t act_r = make_rsrc(action, (uint64_t)NA * plane);
     const uint32_t v0_off = NS * plane, cw_off = (NS + 1) * plane, ret_off = (NS + 2) * plane;
-#if RR_STAMPS
-    uint64_t stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rt0_;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0_)::"memory");
-#endif
-    RR_STAMP(0);
 
     // ---- all loads first (one memory round trip per wave); the counter word first, so the
     // reset candidate below is drawn while the state planes are still in flight ----
     uint32_t cw = use_counter ? bld_u(st_r, vo, cw_off) : 0u;
-    float y0[NS], y1[NS], f0[NS], a[NA];
-    if constexpr (ASOA) {
-#pragma unroll
-        for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
-    } else if constexpr (NA == 3 && RR_DIAG == 11) {  // action not loaded (timing probe)
-        a[0] = 0.1f * (float)(lane & 3);
-        a[1] = -0.1f;
-        a[2] = 0.3f;
-    } else if constexpr (NA == 3) {
-        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)((vo << 1) + vo), 0, RR_LD_AUX);  // 12 B rows
-        a[0] = __uint_as_float(v.x);
-        a[1] = __uint_as_float(v.y);
-        a[2] = __uint_as_float(v.z);
-    } else {
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(vo << 1), 0, RR_LD_AUX);  // 8 B rows
-        a[0] = __uint_as_float(v.x);
-        a[1] = __uint_as_float(v.y);
-    }
-#if RR_DIAG == 3
-#pragma unroll
-    for (int j = 0; j < NS; ++j) y0[j] = P.ic_low[j] + P.ic_span[j] * (float)(lane & 15) * (1.0f / 16.0f);
-#else
+    float y0[NS], y1[NS], a[NA];
+    load_action<NA, ASOA>(make_rsrc(action, (uint64_t)NA * plane), vo, plane, a);
 #pragma unroll
     for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
-#endif
-#if RR_DIAG == 10  // v0 not loaded (timing probe: is the last load's arrival critical?)
-    float v0 = 50.0f + (float)(lane & 7);
-#else
     float v0 = bld_f(st_r, vo, v0_off);
-#endif
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
-#if RR_EARLY_RESET
     // SB3 auto-reset candidate of this step, keyed on (gid, counter word): ~190 VALU right
     // after the counter word lands, instead of in the done branch of the waves that finish
     // last. Used by done lanes only. (HELP: drawn by the helper wave instead.)
@@ -1157,71 +1183,14 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
         ResetStream key = reset_stream(P.seed_w, P.id_off + i, cw);
         sample_ic<MODEL>(P, key, ic_s, ic_v0);
     }
-#endif
-#if RR_DIAG == 4
-    {  // force every load to land, then stamp
-        float sum_ = v0 + (float)cw + ret;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) sum_ += y0[j];
-#pragma unroll
-        for (int j = 0; j < NA; ++j) sum_ += a[j];
-        asm volatile("" ::"v"(sum_));
-    }
-#endif
-    RR_STAMP(1);
 
-#if RR_DIAG == 1
-#pragma unroll
-    for (int j = 0; j < NS; ++j) y1[j] = y0[j] + 1e-7f * a[j % NA];
-    const bool event = false;
-#else
-    const Ctl c = make_ctl<MODEL>(P, a);
-    integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
-    const float g0 = y0[EV], g1 = y1[EV];
-#if RR_DIAG == 2 || RR_DIAG == 5
-    const bool event = false;
-#else
-    const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
-#endif
-    RR_STAMP(2);
-    if (event) event_step<MODEL>(P, c, y0, f0, y1);
-#endif
-    RR_STAMP(3);
-
-    post_integrate<MODEL>(y1);
-
+    const bool event = physics_step<MODEL, INTEG>(P, a, y0, y1);
     bool bv;
     float t[NT];
-#if RR_DIAG == 1
-    bv = y1[0] > 1e30f;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) t[j] = 0.0f;
-    float r = v0;
-#elif RR_DIAG == 9  // reward terms skipped (bounds kept): the reward's share of the launch
-    bv = bounds_hit<MODEL>(H, y1);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) t[j] = 0.0f;
-    float r = v0 + a[0];
-#else
-    float r = reward_terms<MODEL>(H, y1, a, v0, bv, t);
-#endif
-#if RR_DIAG == 2
-    bool done = false;
-#else
-    bool done = event || bv;
-#endif
-
-    // gym TimeLimit (main_6DOF.py:67): elapsed += 1; at the limit done = True and
-    // info["TimeLimit.truncated"] = not done
-    bool trunc = false;
-    int32_t el = (int32_t)(cw & kElapsedMask) + 1;
-    if (P.max_steps > 0 && el >= P.max_steps) {
-        trunc = !done;
-        done = true;
-    }
+    const float r = reward_terms<MODEL>(H, y1, a, v0, bv, t);
+    bool done = event || bv, trunc;
+    int32_t el = time_limit(P, cw, done, trunc);
     ret += r;
-    RR_STAMP(4);
-
     float o[NS];
     normalize_obs<NS>(y1, H.inv_norm, o);
 
@@ -1230,34 +1199,10 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     // side expands the masks into the sorted index list, rr_fetch_done).
     const bool dv = done && valid;
     const uint64_t m = __ballot(dv);
-    if (lane == 0) {
-        if constexpr (EPW == kWave) B.done_bits[wave_idx] = m;
-        else reinterpret_cast<uint32_t*>(B.done_bits)[wave_idx] = (uint32_t)m;  // little-endian: same bit order
-    }
+    if (lane == 0) B.done_bits[wave_idx] = m;
     if (m) {
-        if (dv) {
-            // row i of [N][NS]: 16-B stores (rows are 4-B aligned; gfx950 buffer stores
-            // need only dword alignment), NS = 14 -> 3 x 16 B + 8 B, NS = 7 -> 16 B + 12 B
-            const rsrc_t tr = make_rsrc(B.term_obs, (uint64_t)NS * plane);
-            const uint32_t ro = NS == 14 ? (i << 6) - (i << 3) : i * (NS * 4u);  // i * 56 without v_mul_lo_u32
-            auto u4 = [&](int j) {
-                return u32x4{__float_as_uint(o[j]), __float_as_uint(o[j + 1]), __float_as_uint(o[j + 2]),
-                             __float_as_uint(o[j + 3])};
-            };
-#pragma unroll
-            for (int j = 0; j + 4 <= NS; j += 4) __builtin_amdgcn_raw_buffer_store_b128(u4(j), tr, (int)(ro + j * 4), 0, 0);
-            if constexpr (NS % 4 == 2)
-                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
-                                                      (int)(ro + (NS - 2) * 4), 0, 0);
-            else if constexpr (NS % 4 == 3)
-                __builtin_amdgcn_raw_buffer_store_b96(
-                    u32x3{__float_as_uint(o[NS - 3]), __float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
-                    (int)(ro + (NS - 3) * 4), 0, 0);
-            bst_f<0>(make_rsrc(B.term_ret, plane), ret, vo, 0);
-            bst_u<0>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
-        }
-        if ((mode & RR_FLAG_AUTO_RESET) && dv && RR_DIAG != 6) {
-            const uint32_t ep = (cw >> kEpisodeShift) + 1u;
+        if (dv) store_terminal<NS>(B, i, vo, plane, o, ret, el);
+        if ((mode & RR_FLAG_AUTO_RESET) && dv) {
             if constexpr (HELP) {
                 while (__hip_atomic_load(&cflag[wv], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
                     __builtin_amdgcn_s_sleep(1);
@@ -1266,66 +1211,29 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
                 for (int j = 0; j < NS; ++j) y1[j] = row[j];
                 v0 = row[NS];
             } else {
-#if RR_EARLY_RESET
 #pragma unroll
-            for (int j = 0; j < NS; ++j) y1[j] = ic_s[j];
-            v0 = ic_v0;
-#else
-            ResetStream key = reset_stream(P.seed_w, P.id_off + i, cw);
-            sample_ic<MODEL>(P, key, y1, v0);
-#endif
+                for (int j = 0; j < NS; ++j) y1[j] = ic_s[j];
+                v0 = ic_v0;
             }
             bst_f(st_r, v0, vo, v0_off);
-            cw = ep << kEpisodeShift;
+            cw = ((cw >> kEpisodeShift) + 1u) << kEpisodeShift;
             normalize_obs<NS>(y1, H.inv_norm, o);
             el = 0;
             ret = 0.0f;
         }
     }
     cw = (cw & ~kElapsedMask) | ((uint32_t)el & kElapsedMask);
-    RR_STAMP(5);
 
     if (valid) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
         if (use_counter) bst_u(st_r, cw, vo, cw_off);
         if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, ret_off);
-        bst_f<RR_OUT_AUX>(make_rsrc(io.reward, plane), r, vo, 0);
-        bst_u8<RR_OUT_AUX>(make_rsrc(io.done, n), (uint8_t)done, i);
-        if (io.truncated) bst_u8<RR_OUT_AUX>(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
-        if (io.terms) {
-            const rsrc_t tr = make_rsrc(io.terms, (uint64_t)(NT + 2) * plane);
-#pragma unroll
-            for (int j = 0; j < NT; ++j) bst_f(tr, t[j], vo, j * plane);
-            bst_f(tr, bv ? 1.0f : 0.0f, vo, NT * plane);           // info["bounds_violation"]
-            bst_f(tr, event ? 1.0f : 0.0f, vo, (NT + 1) * plane);  // solve_ivp status == 1
-        }
+        store_outputs<NT>(io, i, vo, plane, n, r, done, trunc, t, bv, event);
     }
-    const uint32_t nvalid = (n - wave_base) < (uint32_t)EPW ? (n - wave_base) : (uint32_t)EPW;
-    store_obs_tile<NS, EPW>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
-                            io.obs_vec_ok);
-    RR_STAMP(6);
-#if RR_DIAG == 12
-    stamp_[0] = __popcll(__ballot(event && valid));
-    stamp_[1] = __popcll(m);
-#endif
-#if RR_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    RR_STAMP(7);
-    uint64_t rt1_;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1_)::"memory");
-    uint32_t xcc_, hwid_;  // placement of this wave
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid_));
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) B.stamps[(size_t)wave_idx * 12 + k] = stamp_[k];
-        B.stamps[(size_t)wave_idx * 12 + 8] = rt0_;
-        B.stamps[(size_t)wave_idx * 12 + 9] = rt1_;
-        B.stamps[(size_t)wave_idx * 12 + 10] = xcc_;
-        B.stamps[(size_t)wave_idx * 12 + 11] = hwid_;
-    }
-#endif
+    const uint32_t nvalid = (n - wave_base) < (uint32_t)kWave ? (n - wave_base) : (uint32_t)kWave;
+    store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
+                              io.obs_vec_ok);
 }
 
 template <int MODEL>
@@ -1539,9 +1447,6 @@ struct rr_env {
     float* term_ret;
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
-#if RR_STAMPS
-    uint64_t* stamps;
-#endif
     int32_t* g_idx;     // rr_fetch_done scratch
     float* g_obs;
     float* g_ret;
@@ -1558,9 +1463,6 @@ Bufs bufs_of(const rr_env* e)
     b.counter = e->counter;
     b.ep_ret = e->ep_ret;
     b.done_bits = e->done_bits;
-#if RR_STAMPS
-    b.stamps = e->stamps;
-#endif
     b.term_obs = e->term_obs;
     b.term_ret = e->term_ret;
     b.term_len = e->term_len;
@@ -1633,9 +1535,6 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->term_ret, sizeof(float) * n},        {(void**)&e->term_len, sizeof(int32_t) * n},
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
-#if RR_STAMPS
-        {(void**)&e->stamps, sizeof(uint64_t) * 12 * n_words(n)},
-#endif
     };
     const bool exact = p->integrator == RR_INT_DOPRI5;
     for (auto& a : allocs) {
@@ -1714,11 +1613,13 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_reset: launch");
 }
 
-int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
-            float* terms, void* stream)
+}  // extern "C"
+
+namespace {
+// one step launch (rr_step / rr_step_repeat; arguments checked by the caller)
+int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
+                float* terms, void* stream)
 {
-    if (!e) return fail(RR_EINVAL, "rr_step: null handle");
-    if (!action || !obs || !reward || !done) return fail(RR_EINVAL, "rr_step: action/obs/reward/done required");
     StepIO io;
     io.action = action;
     io.obs = obs;
@@ -1744,10 +1645,10 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
         const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;
         // up to 16 384 envs one main wave per workgroup (64 + 64 threads): the few workgroups
         // spread over 4x as many CUs (A/B at N = 4 096: -5 % 6DOF); above, 4 main waves
-        const bool wide = e->n <= RR_NARROW_MAX_N;
+        const bool narrow = e->n <= RR_NARROW_MAX_N;
 #define RR_LAUNCH(M, I, A)                                                                                          \
     do {                                                                                                             \
-        if (help && wide)                                                                                            \
+        if (help && narrow)                                                                                          \
             hipLaunchKernelGGL((step_kernel<M, I, A, true, 1>), dim3((unsigned)((e->n + kWave - 1) / kWave)),       \
                                dim3(2 * kWave), 0, s, e->state, action, nn, mode, e->kp, b, io);                     \
         else if (help)                                                                                               \
@@ -1775,6 +1676,31 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return hip_fail(err, "rr_step: launch");
     e->steps++;
+    return RR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
+            float* terms, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_step: null handle");
+    if (!action || !obs || !reward || !done) return fail(RR_EINVAL, "rr_step: action/obs/reward/done required");
+    return launch_step(e, action, obs, reward, done, truncated, terms, stream);
+}
+
+int rr_step_repeat(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs, float* reward,
+                   uint8_t* done, uint8_t* truncated, float* terms, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_step_repeat: null handle");
+    if (!actions || !obs || !reward || !done) return fail(RR_EINVAL, "rr_step_repeat: actions/obs/reward/done required");
+    if (n_batches <= 0 || n_steps < 0) return fail(RR_EINVAL, "rr_step_repeat: n_batches must be >= 1, n_steps >= 0");
+    const int64_t batch = e->n * e->na;
+    for (int64_t t = 0; t < n_steps; ++t) {
+        const int rc = launch_step(e, actions + (t % n_batches) * batch, obs, reward, done, truncated, terms, stream);
+        if (rc != RR_OK) return rc;
+    }
     return RR_OK;
 }
 
@@ -2191,15 +2117,5 @@ int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, cons
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_gae: launch");
 }
 
-#if RR_STAMPS
-// diagnostic build only: copy the per-wave phase stamps of the last step to the host
-int64_t rr_debug_stamps(rr_env* e, uint64_t* host, int64_t cap)
-{
-    const int64_t nw = std::min<int64_t>(cap / 12, n_words(e->n));
-    hipError_t err = hipDeviceSynchronize();
-    if (err == hipSuccess) err = hipMemcpy(host, e->stamps, sizeof(uint64_t) * 12 * nw, hipMemcpyDeviceToHost);
-    return err == hipSuccess ? nw : hip_fail(err, "rr_debug_stamps");
-}
-#endif
 
 }  // extern "C"

@@ -163,12 +163,14 @@ def test_full_size_properties_6dof():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model", [6, 3])
-@pytest.mark.parametrize("n", [65536 + 300, 4096 + 37])
-def test_helper_wave_launch_is_bitwise_equal(model, n, monkeypatch):
+@pytest.mark.parametrize("n,auto_reset", [(65536 + 300, True), (4096 + 37, True), (65536 + 300, False)])
+def test_helper_wave_launch_is_bitwise_equal(model, n, auto_reset, monkeypatch):
     """At small N the step kernel runs with helper waves that draw the auto-reset candidates
-    (step_kernel<..., HELP = true, WPB>, rr_create reads RR_HELP_MAX_N). Outputs, terminal
-    rows and state must be bitwise those of the single-role kernel, over steps with many
-    resets. Ragged last workgroup; N = 4096 + 37 runs one main wave per workgroup (WPB = 1)."""
+    (step_kernel<..., HELP = true, WPB>, rr_create reads RR_HELP_MAX_N). Outputs, reward
+    terms, terminal rows, Monitor returns and state must be bitwise those of the single-role
+    kernel, over steps with many resets. Ragged last workgroup; N = 4096 + 37 runs one main
+    wave per workgroup (WPB = 1); without auto-reset both launches are the single-role kernel
+    (a check of the test itself)."""
     import torch
     from rl_rocket_amd.batch import RocketBatch
 
@@ -176,7 +178,8 @@ def test_helper_wave_launch_is_bitwise_equal(model, n, monkeypatch):
 
     def run(help_max_n):
         monkeypatch.setenv("RR_HELP_MAX_N", str(help_max_n))
-        b = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=40, **kw)
+        b = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=40, auto_reset=auto_reset,
+                        compute_terms=True, **kw)
         b.reset()
         gen = torch.Generator(device="cuda:0")
         gen.manual_seed(7)
@@ -186,7 +189,10 @@ def test_helper_wave_launch_is_bitwise_equal(model, n, monkeypatch):
             obs, rew, done, trunc = b.step(a)
             idx, tobs, ret, ln = b.fetch_done()
             resets += len(idx)
-            out.append((obs.clone(), rew.clone(), done.clone(), trunc.clone(), torch.as_tensor(tobs).clone()))
+            out.append((obs.clone(), rew.clone(), done.clone(), trunc.clone(), b.terms.clone(),
+                        torch.as_tensor(tobs).clone(), torch.as_tensor(ret).clone(), torch.as_tensor(ln).clone()))
+            if not auto_reset and len(idx):
+                b.reset(done)
         st = b.get_state()
         torch.cuda.synchronize()
         b.close()
@@ -194,7 +200,7 @@ def test_helper_wave_launch_is_bitwise_equal(model, n, monkeypatch):
 
     h_help, st_help, resets = run(1 << 40)
     h_plain, st_plain, _ = run(0)
-    assert resets >= n  # TimeLimit 40 over 60 steps: every env reset at least once
+    assert resets >= n  # TimeLimit 40 over 60 steps: every env done at least once
     for x, y in zip(h_help, h_plain):
         for u, v in zip(x, y):
             assert torch.equal(u, v)

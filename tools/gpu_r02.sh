@@ -1,0 +1,45 @@
+#!/bin/bash
+# One GPU session (round 2 protocol): parity tests, smoke, the driver's bench protocol
+# (--steps 20 --warmup 5) plus the long form, rocprofv3 kernel-trace stats of the driver's
+# command, SQ issue counters and HBM traffic counters in their own passes.
+# Every GPU step has its own timeout; a crash / timeout / abort ends the script.
+# Usage: tools/gpu_r02.sh TAG      env: TESTS=0 skips pytest, PMC=0 skips counter passes,
+#                                       BENCH_ARGS="..." extra bench.py args for every bench leg
+TAG=${1:-run}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 2
+OUT="$R/gpurun_out/$TAG"
+mkdir -p "$OUT"
+step() {  # step NAME TIMEOUT cmd...: 0 = ok, 1 = test failures (continue), anything else = stop
+  local name=$1 to=$2; shift 2
+  echo "[$name] start $(date +%T)"
+  timeout -k 10 "$to" "$@"
+  local rc=$?
+  echo "[$name] exit $rc" | tee -a "$OUT/status.txt"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
+}
+git -C "$R" rev-parse HEAD > "$OUT/head.txt" 2>/dev/null || true
+if [ "${TESTS:-1}" = 1 ]; then
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+  tail -3 "$OUT/pytest_gpu.log"
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+fi
+for i in 1 2 3; do
+  step bench_k20_$i 300 python bench.py --steps 20 --warmup 5 $BENCH_ARGS > "$OUT/bench_k20_$i.json" 2> "$OUT/bench_k20_$i.err"
+  cat "$OUT/bench_k20_$i.json"
+done
+step bench_k2000 300 python bench.py --no-cpu-baseline $BENCH_ARGS > "$OUT/bench_k2000.json" 2> "$OUT/bench_k2000.err"
+cat "$OUT/bench_k2000.json"
+export TMPDIR=/tmp
+cd /tmp || exit 2
+step rocprof_k20 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_k20" -o bench -- python "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_k20.log" 2>&1
+step rocprof_k2000 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_k2000" -o bench -- python "$R/bench.py" --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_k2000.log" 2>&1
+if [ "${PMC:-1}" = 1 ]; then
+  step pmc_SQ 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmc_SQ" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $BENCH_ARGS > "$OUT/pmc_SQ.log" 2>&1
+  step pmc_SQ2 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32 --output-format csv -d "$OUT/pmc_SQ2" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $BENCH_ARGS > "$OUT/pmc_SQ2.log" 2>&1
+  step pmc_GRBM 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmc_GRBM" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $BENCH_ARGS > "$OUT/pmc_GRBM.log" 2>&1
+  for C in FETCH_SIZE WRITE_SIZE; do
+    step pmc_$C 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $BENCH_ARGS > "$OUT/pmc_$C.log" 2>&1
+  done
+fi
+echo done
