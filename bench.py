@@ -232,7 +232,12 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    if world == 1 and args.allgather:  # step + gather path on one GPU (a rehearsal of the collective)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29571")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or args.allgather:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -264,9 +269,12 @@ def main():
         gather = ShardGather(n, env.state_dim, dev)
 
     def one(k):
-        obs, rew, done, _ = env.step(pool[k % POOL])
         if gather is not None:
-            gather(obs, rew, done)  # RCCL all_gather over xGMI: global batch on every rank
+            # the step writes obs / reward / done straight into the send rows (rr_step_rows),
+            # then ONE RCCL all_gather over xGMI: the global batch on every rank
+            gather.step(env, pool[k % POOL])
+        else:
+            env.step(pool[k % POOL])
 
     stream = torch.cuda.current_stream(dev)
     for k in range(args.warmup):
@@ -274,7 +282,8 @@ def main():
     torch.cuda.synchronize(dev)
 
     # ---- timed region: exactly K steps (hipGraph replays) ----
-    use_graph = not args.no_graph and not args.allgather and args.launch == "graph"
+    # step + all_gather graphs need a capturable collective (RCCL); gloo is a host path
+    use_graph = not args.no_graph and args.launch == "graph" and not (gather is not None and backend == "gloo")
     use_loop = args.launch == "loop" and not args.allgather
     # exactly K steps: K // gs replays of a gs-launch graph (gs balanced so that K = 2000 is
     # 2 x 1000, not 1024 + 976) plus one graph of the K % gs remainder launches
@@ -289,7 +298,7 @@ def main():
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 for k in range(n_launch):
-                    env.step(pool[k % POOL])
+                    one(k)
         stream.wait_stream(s)
         torch.cuda.synchronize(dev)
         g.replay()  # warm the graph
@@ -352,7 +361,7 @@ def main():
                 "batches resident in HBM" % POOL,
         "config": {"workload": "Rocket%s N=%d per GPU, %s fused step+reward+TimeLimit(800)+auto-reset, %s"
                                % ("6DOF" if model == 6 else "3DOF", n, args.integrator.upper(),
-                                  "RCCL all_gather of obs/reward/done each step" if args.allgather else
+                                  "step rows + RCCL all_gather of obs/reward/done each step" if args.allgather else
                                   "no data-path collective"),
                    "envs_per_gpu": n, "global_envs": n * world, "integrator": args.integrator,
                    "graph_steps": gs if use_graph else 0, "launch": "graph" if use_graph else
@@ -363,7 +372,9 @@ def main():
                      "traffic_source": traffic_src,
                      "kernel": "step_kernel<%d,%s>" % (model, args.integrator.upper()),
                      "kernel_us": kern_ms * 1e3,
-                     "timing": "HIP events on the launch stream around the K launches of the timed region",
+                     "timing": "HIP events on the launch stream around the K launches of the timed region" +
+                               (" (each step = rr_step_rows + the RCCL all_gather, so kernel_us includes the "
+                                "collective)" if gather is not None else ""),
                      "bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": BYTES_PER_STEP[model]},
     }

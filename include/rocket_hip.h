@@ -13,7 +13,7 @@
  *                     (+ seed(): rocket_env.py:1063-1065 / :478-480)
  *   rr_step        <- Rocket6DOF.step rocket_env.py:690-719 (+ Simulator6DOF.step/RHS
  *                     simulator.py:227-378) / Rocket.step :150-175 (+ simulator.py:55-130),
- *                     fused with gym TimeLimit (main_6DOF.py:67), the SB3 vec-env auto-reset
+ *                     fused with gym TimeLimit (main_6DOF.py:21), the SB3 vec-env auto-reset
  *                     and, optionally, RewardAnnealing (wrappers.py:68-86)
  *   rr_set_state / rr_get_state
  *                  <- direct access to Simulator*.state / .t used by the reference's
@@ -21,7 +21,7 @@
  *                     injection and checkpoint/restore)
  *   rr_fetch_done / rr_copy_terminal / rr_get_buffers
  *                  <- info["terminal_observation"] / Monitor episode stats for done envs
- *                     (SB3 DummyVecEnv / Monitor around main_6DOF.py:64-70)
+ *                     (SB3 DummyVecEnv / Monitor, main_6DOF.py:18-24)
  *
  * Conventions
  *   - All data pointers are DEVICE pointers (e.g. torch.Tensor.data_ptr()) on the
@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 4
+#define RR_ABI_VERSION 5
 
 /* error codes */
 #define RR_OK 0
@@ -105,7 +105,8 @@ typedef struct rr_params {
 typedef struct rr_buffers {
     float* state;          /* [state_dim][N] fp32 SoA */
     float* v0;             /* [N] ||IC velocity|| of the episode (rocket_env.py:989-991) */
-    int32_t* elapsed;      /* [N] counter word: TimeLimit steps (bits 0-15) | episode (bits 16-31) */
+    int32_t* elapsed;      /* [N] counter word: TimeLimit steps in bits 0..E-1, episode in bits E..31,
+                              E = rr_counter_bits() */
     float* ep_return;      /* [N] running episode return (RR_FLAG_EPISODE_STATS) */
     uint64_t* done_bits;   /* [ceil(N/64)] wave-ballot done masks: bit b of word w <=> env 64w+b done */
     float* terminal_obs;   /* [N][state_dim] final obs of env i, valid where done[i] */
@@ -127,10 +128,13 @@ int64_t rr_num_envs(const rr_env* e);
 int rr_state_dim(const rr_env* e);
 int rr_action_dim(const rr_env* e);
 
-/* Set the key of the reset stream. Resets are counter-based: env `gid` starting its
- * episode `e` draws its initial condition from a splitmix64 key + 32-bit mixer keyed on
- * (seed, gid, e, bits of the state it replaces) — deterministic, independent of how
- * envs are sharded over GPUs, and free of per-env RNG state in HBM. Host-only call. */
+/* Set the key of the reset stream. Resets are counter-based: when env `gid` ends an episode
+ * with counter word `cw` (episode number | elapsed steps), its next initial condition comes
+ * from a register-resident xorshift128 whose four words are chained lowbias32 mixes of
+ * (the seed's four key words — splitmix64 of `seed` on the host — , gid, cw): deterministic,
+ * independent of how envs are sharded over GPUs, and free of per-env RNG state in HBM. The
+ * episode field has 32 - rr_counter_bits() bits (22 under the reference's TimeLimit 800), so
+ * one env's keys do not repeat for 2^22 episodes. Host-only call. */
 int rr_seed(rr_env* e, uint64_t seed, void* stream);
 /* Sample a fresh initial condition for every env where mask[i] != 0 (all when mask is
  * NULL), write the normalised obs [N][state_dim] (obs may be NULL). */
@@ -149,6 +153,14 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream);
 int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
             float* terms, void* stream);
 
+/* rr_step with obs, reward and done packed as one fp32 row per env: rows [N][state_dim + 2]
+ * = (obs[state_dim], reward, done ? 1 : 0), bitwise the values rr_step writes. One 16-B
+ * coalesced tile store per wave, and the row block is exactly the send buffer of the
+ * multi-GPU all-gather (rl_rocket_amd.dist.ShardGather), so no copy kernels
+ * sit between the step and the collective. truncated / terms as rr_step. RK4 / Euler envs
+ * with [N][action_dim] actions. */
+int rr_step_rows(rr_env* e, const float* action, float* rows, uint8_t* truncated, float* terms, void* stream);
+
 /* n_steps consecutive rr_step launches on `stream`, step t taking action batch t % n_batches
  * of `actions` ([n_batches][N][action_dim], or [n_batches][action_dim][N] planes with
  * RR_FLAG_ACTION_SOA) — open-loop action sequences already resident on the device (e.g. a
@@ -159,8 +171,12 @@ int rr_step_repeat(rr_env* e, const float* actions, int64_t n_batches, int64_t n
 
 /* Overwrite / read the per-env state (parity injection, checkpoint / restore).
  * state_soa [state_dim][N] fp32; v0 [N] or NULL (kept on set / skipped on get);
- * elapsed [N] or NULL (zeroed on set / skipped on get) is the per-env counter word:
- * TimeLimit steps in bits 0-15, episodes started in bits 16-31 (keys the reset stream). */
+ * elapsed [N] or NULL is the per-env counter word: TimeLimit steps in bits 0..E-1, episodes
+ * started in bits E..31 (keys the reset stream), E = rr_counter_bits(e); a plain step count
+ * is a valid word (episode 0). On set, NULL clears the steps and keeps the episode field.
+ * rr_set_state* zero the Monitor running return (an injected state starts a new segment);
+ * rr_get_aux / rr_set_aux round-trip the raw counter words and the running return for a
+ * checkpoint. */
 int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32_t* elapsed, void* stream);
 int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void* stream);
 /* Same with an fp64 state [state_dim][N]. Under RR_INT_DOPRI5 this is the state the
@@ -168,6 +184,11 @@ int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void*
  * to / from the fp32 planes. In DOPRI5 mode elapsed also sets the clock: t = steps*dt. */
 int rr_set_state64(rr_env* e, const double* state_soa, const float* v0, const int32_t* elapsed, void* stream);
 int rr_get_state64(rr_env* e, double* state_soa, float* v0, int32_t* elapsed, void* stream);
+/* Bits E of the elapsed-steps field of the counter word (16 without a TimeLimit). */
+int rr_counter_bits(const rr_env* e);
+/* Raw counter words [N] and Monitor running returns [N] (either may be NULL). */
+int rr_get_aux(rr_env* e, uint32_t* counter, float* ep_return, void* stream);
+int rr_set_aux(rr_env* e, const uint32_t* counter, const float* ep_return, void* stream);
 
 /* Pointers to the library-owned buffers (done list of the last step, etc.). */
 int rr_get_buffers(rr_env* e, rr_buffers* out);
@@ -186,7 +207,7 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
 
 /* ---- On-device PPO rollouts (BASELINE configs[4]) ----
  * Replace the per-step host work of stable_baselines3 1.6 OnPolicyAlgorithm.collect_rollouts
- * + RolloutBuffer (the reference trains PPO("MlpPolicy", ...), main_6DOF.py:110-116) for
+ * + RolloutBuffer (the reference trains PPO("MlpPolicy", ...), main_6DOF.py:62-69) for
  * an on-device rollout: the MlpPolicy actor-critic (separate pi / vf towers, net_arch
  * [64, 64], tanh, state-independent log_std) runs as one fp32 MFMA launch per step.
  * Supported (obs_dim, act_dim): (14, 3) 6DOF, (7, 2) 3DOF.
@@ -253,7 +274,7 @@ int rr_rollout_step(rr_env* e, const float* params, int precision, uint64_t seed
 
 /* A whole PPO rollout in ONE launch (replaces SB3 OnPolicyAlgorithm.collect_rollouts +
  * RolloutBuffer.compute_returns_and_advantage, stable_baselines3 1.6 on_policy_algorithm.py /
- * buffers.py, driving the reference's env through main_6DOF.py:60-120). Steps t = 0..n_steps-1
+ * buffers.py, driving the reference's env through main_6DOF.py:60-103). Steps t = 0..n_steps-1
  * are exactly rr_rollout_step(t) — same noise key (seed, env id, *iter, t), same env step,
  * bootstrap and buffer writes, now into the [t] slices of [n_steps][n] buffers — with the env
  * state kept in registers between steps; then last_value[i] = V(post-step obs) (as

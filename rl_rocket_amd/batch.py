@@ -95,6 +95,21 @@ class RocketBatch:
                                     _ptr(self.truncated), _ptr(self.terms), self._stream()), "rr_step")
         return self.obs, self.reward, self.done, self.truncated
 
+    def step_rows(self, action, rows):
+        """One env step writing obs, reward and done as rows [N, state_dim + 2] fp32 (obs,
+        reward, done 0 / 1) into the device tensor `rows` (rr_step_rows; e.g. an all-gather
+        send buffer). Returns `rows`; truncated / terms as step()."""
+        t = self.torch
+        if rows.shape != (self.num_envs, self.state_dim + 2) or rows.dtype != t.float32 or not rows.is_contiguous() \
+                or rows.device != self.device:
+            raise ValueError("rows must be a contiguous float32 [%d, %d] tensor on %s"
+                             % (self.num_envs, self.state_dim + 2, self.device))
+        action = self._check_action(action)
+        self._last_action = action
+        _lib.check(self.lib.rr_step_rows(self._h, _ptr(action), _ptr(rows), _ptr(self.truncated), _ptr(self.terms),
+                                         self._stream()), "rr_step_rows")
+        return rows
+
     def step_repeat(self, actions, n_steps):
         """`n_steps` consecutive steps, step t taking action batch t % len(actions) of the device
         tensor `actions` [B][N][action_dim] (rr_step_repeat: one host call). Returns the output
@@ -111,6 +126,9 @@ class RocketBatch:
         return self.obs, self.reward, self.done, self.truncated
 
     def set_state(self, state_soa, v0=None, elapsed=None):
+        """Inject fp32 state planes [state_dim][N]; v0 [N] (kept when None); `elapsed` = counter
+        words [N] (a plain step count is episode 0; None clears the steps and keeps the episode
+        field). Zeroes the Monitor running return (restore() keeps it)."""
         t = self.torch
         st = t.as_tensor(state_soa, device=self.device, dtype=t.float32).reshape(self.state_dim, self.num_envs)
         st = st.contiguous()
@@ -126,6 +144,42 @@ class RocketBatch:
         el = t.empty((self.num_envs,), dtype=t.int32, device=self.device)
         _lib.check(self.lib.rr_get_state(self._h, _ptr(st), _ptr(v), _ptr(el), self._stream()), "rr_get_state")
         return st, v, el
+
+    # -- counter words and checkpoints ---------------------------------------------------------------------------
+    @property
+    def counter_bits(self):
+        """Bits E of the elapsed-steps field of the counter word (episode number in bits E..31)."""
+        return _lib.check(self.lib.rr_counter_bits(self._h), "rr_counter_bits")
+
+    def split_counter(self, counter):
+        """(elapsed steps, episode number) of counter words (tensor or array)."""
+        e = self.counter_bits
+        c = counter.to(self.torch.int64) & 0xFFFFFFFF if isinstance(counter, self.torch.Tensor) else \
+            np.asarray(counter).astype(np.int64) & 0xFFFFFFFF
+        return c & ((1 << e) - 1), c >> e
+
+    def make_counter(self, elapsed, episode=0):
+        """Counter words from elapsed steps and episode numbers (int32 view of the u32 word)."""
+        e = self.counter_bits
+        w = (np.asarray(episode, np.int64) << e) | np.asarray(elapsed, np.int64)
+        return (w & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+
+    def checkpoint(self):
+        """Everything a restore needs, as device tensors: state planes, v0, raw counter words
+        (TimeLimit steps | episode: keys the reset stream) and Monitor running returns."""
+        t = self.torch
+        st, v0, _ = self.get_state()
+        cw = t.empty((self.num_envs,), dtype=t.int32, device=self.device)
+        ret = t.empty((self.num_envs,), dtype=t.float32, device=self.device)
+        _lib.check(self.lib.rr_get_aux(self._h, _ptr(cw), _ptr(ret), self._stream()), "rr_get_aux")
+        return {"state": st, "v0": v0, "counter": cw, "ep_return": ret}
+
+    def restore(self, ck):
+        """Inverse of checkpoint(): the next steps are bitwise those of the checkpointed env."""
+        self.set_state(ck["state"], v0=ck["v0"], elapsed=ck["counter"])
+        cw, ret = ck["counter"].contiguous(), ck["ep_return"].contiguous()
+        self._keep_aux = (cw, ret)
+        _lib.check(self.lib.rr_set_aux(self._h, _ptr(cw), _ptr(ret), self._stream()), "rr_set_aux")
 
     def set_state64(self, state_soa, v0=None, elapsed=None):
         """fp64 state [state_dim][N] (the integrator's own state under integrator="dopri5";

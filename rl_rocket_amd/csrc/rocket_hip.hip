@@ -100,10 +100,11 @@ constexpr float kLeverOverI3 = (float)(kLever3 / kI3);
 constexpr float kHalfPi = 1.57079632679489662f;
 constexpr float kTwoPi = 6.28318530717958648f;
 
-// Per-env counter word: TimeLimit steps in the low 16 bits, episodes started in the
-// high 16 bits (keys the counter-based reset stream).
-constexpr uint32_t kElapsedMask = 0xFFFFu;
-constexpr int kEpisodeShift = 16;
+// Per-env counter word: TimeLimit steps in the low E bits, episodes started in the high
+// 32 - E bits (keys the counter-based reset stream). E = bits of max_episode_steps (10 for the
+// reference's TimeLimit 800: 2^22 episodes per env before the episode field wraps), 16 without
+// a TimeLimit (KParams.el_mask / ep_shift, counter_bits()).
+constexpr int32_t kMaxEpisodeSteps = 0xFFFF;
 // step_kernel `mode` word: rr_params.flags plus "the counter word is live"
 constexpr uint32_t kModeCounter = 0x80000000u;
 
@@ -111,6 +112,7 @@ constexpr uint32_t kModeCounter = 0x80000000u;
 struct KParams {
     int32_t max_steps;
     uint32_t flags;
+    uint32_t el_mask, ep_shift; // counter word: elapsed = cw & el_mask, episode = cw >> ep_shift
     float h, h2, h6;          // dt, dt/2, dt/6
     float ic_low[RR_MAX_STATE];
     float ic_span[RR_MAX_STATE];
@@ -1053,7 +1055,7 @@ __device__ __forceinline__ bool physics_step(const KParams& P, const float* a, c
 // info["TimeLimit.truncated"] = not done. Returns the new elapsed count.
 __device__ __forceinline__ int32_t time_limit(const KParams& P, uint32_t cw, bool& done, bool& trunc)
 {
-    const int32_t el = (int32_t)(cw & kElapsedMask) + 1;
+    const int32_t el = (int32_t)(cw & P.el_mask) + 1;
     trunc = false;
     if (P.max_steps > 0 && el >= P.max_steps) {
         trunc = !done;
@@ -1088,13 +1090,16 @@ __device__ __forceinline__ void store_terminal(const Bufs& B, uint32_t i, uint32
     bst_u<0>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
 }
 
-// per-env step outputs owned by the caller: reward, done, truncated, optional terms
-template <int NT>
+// per-env step outputs owned by the caller: reward, done (unless they travel in the obs row),
+// truncated, optional terms
+template <int NT, bool REWARD_DONE = true>
 __device__ __forceinline__ void store_outputs(const StepIO& io, uint32_t i, uint32_t vo, uint32_t plane, uint32_t n,
                                               float r, bool done, bool trunc, const float* t, bool bv, bool event)
 {
-    bst_f<RR_OUT_AUX>(make_rsrc(io.reward, plane), r, vo, 0);
-    bst_u8<RR_OUT_AUX>(make_rsrc(io.done, n), (uint8_t)done, i);
+    if constexpr (REWARD_DONE) {
+        bst_f<RR_OUT_AUX>(make_rsrc(io.reward, plane), r, vo, 0);
+        bst_u8<RR_OUT_AUX>(make_rsrc(io.done, n), (uint8_t)done, i);
+    }
     if (io.truncated) bst_u8<RR_OUT_AUX>(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
     if (io.terms) {
         const rsrc_t tr = make_rsrc(io.terms, (uint64_t)(NT + 2) * plane);
@@ -1115,13 +1120,17 @@ __device__ __forceinline__ void store_outputs(const StepIO& io, uint32_t i, uint
 // wave draws the candidate itself right after its counter word lands. Measured and rejected
 // (round 2): a helper that also computes reward, obs and every caller-owned output while the
 // main wave resets and stores the state (bitwise equal, 4.69 vs 4.31 us per step at N = 65536).
-template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB = kWavesPerBlock>
+// ROWS (rr_step_rows): obs, reward and done leave as ONE row of NS + 2 fp32 per env
+// (obs[NS], reward, done as 0 / 1) through the same LDS tile, e.g. straight into the send
+// buffer of the multi-GPU all-gather (rl_rocket_amd.dist.ShardGather).
+template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB, bool ROWS>
 __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR void step_kernel(
     float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
     const Bufs B, const StepIO io)
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT;
-    __shared__ __attribute__((aligned(16))) float lds[WPB][kWave * NS];
+    constexpr int OW = ROWS ? NS + 2 : NS;  // floats per output row
+    __shared__ __attribute__((aligned(16))) float lds[WPB][kWave * OW];
     constexpr int kCandRow = (NS + 1 + 3) / 4 * 4;
     __shared__ __attribute__((aligned(16))) float cand[HELP ? WPB : 1][HELP ? kWave * kCandRow : 1];
     __shared__ uint32_t cflag[WPB];
@@ -1216,24 +1225,34 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
                 v0 = ic_v0;
             }
             bst_f(st_r, v0, vo, v0_off);
-            cw = ((cw >> kEpisodeShift) + 1u) << kEpisodeShift;
+            cw = ((cw >> P.ep_shift) + 1u) << P.ep_shift;
             normalize_obs<NS>(y1, H.inv_norm, o);
             el = 0;
             ret = 0.0f;
         }
     }
-    cw = (cw & ~kElapsedMask) | ((uint32_t)el & kElapsedMask);
+    cw = (cw & ~P.el_mask) | ((uint32_t)el & P.el_mask);
 
     if (valid) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
         if (use_counter) bst_u(st_r, cw, vo, cw_off);
         if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, ret_off);
-        store_outputs<NT>(io, i, vo, plane, n, r, done, trunc, t, bv, event);
+        store_outputs<NT, !ROWS>(io, i, vo, plane, n, r, done, trunc, t, bv, event);
     }
     const uint32_t nvalid = (n - wave_base) < (uint32_t)kWave ? (n - wave_base) : (uint32_t)kWave;
-    store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
-                              io.obs_vec_ok);
+    if constexpr (ROWS) {
+        float ow[OW];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) ow[j] = o[j];
+        ow[NS] = r;
+        ow[NS + 1] = done ? 1.0f : 0.0f;
+        store_obs_tile<OW, kWave>(lds[wv], ow, make_rsrc(io.obs, (uint64_t)OW * plane), wave_base, lane, nvalid,
+                                  io.obs_vec_ok);
+    } else {
+        store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
+                                  io.obs_vec_ok);
+    }
 }
 
 template <int MODEL>
@@ -1246,7 +1265,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
     const int64_t n = B.n;
     float s[NS], v0;
     if (mask == nullptr || mask[i]) {
-        const uint32_t ep = (B.counter[i] >> kEpisodeShift) + 1u;
+        const uint32_t ep = (B.counter[i] >> P.ep_shift) + 1u;
         ResetStream key = reset_stream(P.seed_w, P.id_off + i, B.counter[i]);
         sample_ic<MODEL>(P, key, s, v0);
 #pragma unroll
@@ -1256,7 +1275,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
             for (int j = 0; j < NS; ++j) state64[(int64_t)j * n + i] = (double)s[j];
         }
         B.v0[i] = v0;
-        B.counter[i] = ep << kEpisodeShift;
+        B.counter[i] = ep << P.ep_shift;
         B.ep_ret[i] = 0.0f;
     } else {
 #pragma unroll
@@ -1266,6 +1285,13 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
 #pragma unroll
         for (int j = 0; j < NS; ++j) obs[i * NS + j] = s[j] * P.inv_norm[j];
     }
+}
+
+// counter words: clear the elapsed field, keep the episode field (rr_set_state without elapsed)
+__global__ __launch_bounds__(kBlock) void clear_elapsed_kernel(uint32_t* counter, int64_t n, uint32_t el_mask)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) counter[i] &= ~el_mask;
 }
 
 // Compact the terminal rows of the (sorted) done list for one host copy.
@@ -1337,6 +1363,16 @@ void seed_words(uint64_t seed, uint32_t* w)
     w[3] = (uint32_t)(b >> 32);
 }
 
+// bits of the elapsed field of the counter word: enough for max_episode_steps (TimeLimit
+// 800 -> 10), 16 without a TimeLimit (elapsed then only counts Monitor's episode length)
+int counter_bits(int32_t max_episode_steps)
+{
+    if (max_episode_steps <= 0) return 16;
+    int b = 1;
+    while (((int64_t)1 << b) <= (int64_t)max_episode_steps) ++b;
+    return b;
+}
+
 KParams make_kparams(const rr_params& p)
 {
     KParams k;
@@ -1344,6 +1380,9 @@ KParams make_kparams(const rr_params& p)
     const int ns = p.model == RR_MODEL_6DOF ? 14 : 7;
     k.max_steps = p.max_episode_steps;
     k.flags = p.flags;
+    const int eb = counter_bits(p.max_episode_steps);
+    k.el_mask = (1u << eb) - 1u;
+    k.ep_shift = (uint32_t)eb;
     k.h = (float)p.dt;
     k.h2 = 0.5f * k.h;
     k.h6 = k.h / 6.0f;
@@ -1505,7 +1544,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     const int64_t ns_ = p->model == RR_MODEL_6DOF ? 14 : 7;
     if (n <= 0 || n * (ns_ + 3) * 4 > (int64_t)0xFFFFFFFF)
         return fail(RR_EINVAL, "rr_create: n must be >= 1 and n*state_dim*4 must fit 32-bit buffer offsets");
-    if (p->max_episode_steps < 0 || p->max_episode_steps > (int32_t)kElapsedMask)
+    if (p->max_episode_steps < 0 || p->max_episode_steps > kMaxEpisodeSteps)
         return fail(RR_EINVAL, "rr_create: max_episode_steps must be in [0, 65535]");
     if (!(p->dt > 0.0)) return fail(RR_EINVAL, "rr_create: dt must be > 0");
     rr_env* e = new (std::nothrow) rr_env();
@@ -1617,6 +1656,7 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
 
 namespace {
 // one step launch (rr_step / rr_step_repeat; arguments checked by the caller)
+template <bool ROWS>
 int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
                 float* terms, void* stream)
 {
@@ -1649,16 +1689,21 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
 #define RR_LAUNCH(M, I, A)                                                                                          \
     do {                                                                                                             \
         if (help && narrow)                                                                                          \
-            hipLaunchKernelGGL((step_kernel<M, I, A, true, 1>), dim3((unsigned)((e->n + kWave - 1) / kWave)),       \
+            hipLaunchKernelGGL((step_kernel<M, I, A, true, 1, ROWS>), dim3((unsigned)((e->n + kWave - 1) / kWave)), \
                                dim3(2 * kWave), 0, s, e->state, action, nn, mode, e->kp, b, io);                     \
         else if (help)                                                                                               \
-            hipLaunchKernelGGL((step_kernel<M, I, A, true>), grid, dim3(2 * kBlock), 0, s, e->state, action, nn,    \
-                               mode, e->kp, b, io);                                                                  \
+            hipLaunchKernelGGL((step_kernel<M, I, A, true, kWavesPerBlock, ROWS>), grid, dim3(2 * kBlock), 0, s,     \
+                               e->state, action, nn, mode, e->kp, b, io);                                            \
         else                                                                                                         \
-            hipLaunchKernelGGL((step_kernel<M, I, A, false>), grid, block, 0, s, e->state, action, nn, mode,        \
-                               e->kp, b, io);                                                                        \
+            hipLaunchKernelGGL((step_kernel<M, I, A, false, kWavesPerBlock, ROWS>), grid, block, 0, s, e->state,     \
+                               action, nn, mode, e->kp, b, io);                                                      \
     } while (0)
-        if (m6 && !euler) {
+        if constexpr (ROWS) {  // row-major actions only (the multi-GPU gather path)
+            if (m6 && !euler) RR_LAUNCH(6, RR_INT_RK4, false);
+            else if (m6) RR_LAUNCH(6, RR_INT_EULER, false);
+            else if (!euler) RR_LAUNCH(3, RR_INT_RK4, false);
+            else RR_LAUNCH(3, RR_INT_EULER, false);
+        } else if (m6 && !euler) {
             if (soa) RR_LAUNCH(6, RR_INT_RK4, true);
             else RR_LAUNCH(6, RR_INT_RK4, false);
         } else if (m6) {
@@ -1687,7 +1732,16 @@ int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* 
 {
     if (!e) return fail(RR_EINVAL, "rr_step: null handle");
     if (!action || !obs || !reward || !done) return fail(RR_EINVAL, "rr_step: action/obs/reward/done required");
-    return launch_step(e, action, obs, reward, done, truncated, terms, stream);
+    return launch_step<false>(e, action, obs, reward, done, truncated, terms, stream);
+}
+
+int rr_step_rows(rr_env* e, const float* action, float* rows, uint8_t* truncated, float* terms, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_step_rows: null handle");
+    if (!action || !rows) return fail(RR_EINVAL, "rr_step_rows: action/rows required");
+    if (e->p.integrator == RR_INT_DOPRI5 || (e->p.flags & RR_FLAG_ACTION_SOA))
+        return fail(RR_EINVAL, "rr_step_rows: RK4 / Euler envs with [N][action_dim] actions only");
+    return launch_step<true>(e, action, rows, nullptr, nullptr, truncated, terms, stream);
 }
 
 int rr_step_repeat(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs, float* reward,
@@ -1698,7 +1752,8 @@ int rr_step_repeat(rr_env* e, const float* actions, int64_t n_batches, int64_t n
     if (n_batches <= 0 || n_steps < 0) return fail(RR_EINVAL, "rr_step_repeat: n_batches must be >= 1, n_steps >= 0");
     const int64_t batch = e->n * e->na;
     for (int64_t t = 0; t < n_steps; ++t) {
-        const int rc = launch_step(e, actions + (t % n_batches) * batch, obs, reward, done, truncated, terms, stream);
+        const int rc =
+            launch_step<false>(e, actions + (t % n_batches) * batch, obs, reward, done, truncated, terms, stream);
         if (rc != RR_OK) return rc;
     }
     return RR_OK;
@@ -1712,8 +1767,13 @@ hipError_t set_aux(rr_env* e, const float* v0, const int32_t* elapsed, hipStream
     hipError_t err = hipSuccess;
     if (v0) err = hipMemcpyAsync(e->v0, v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
     if (err == hipSuccess) {
-        if (elapsed) err = hipMemcpyAsync(e->counter, elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
-        else err = hipMemsetAsync(e->counter, 0, sizeof(int32_t) * e->n, s);
+        if (elapsed) {
+            err = hipMemcpyAsync(e->counter, elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+        } else {  // elapsed steps -> 0, the episode field (reset-stream key) is kept
+            hipLaunchKernelGGL(clear_elapsed_kernel, dim3(grid_of(e->n)), dim3(kBlock), 0, s, e->counter, e->n,
+                               e->kp.el_mask);
+            err = hipGetLastError();
+        }
     }
     if (err == hipSuccess) err = hipMemsetAsync(e->ep_ret, 0, sizeof(float) * e->n, s);
     return err;
@@ -1794,6 +1854,30 @@ int rr_get_state64(rr_env* e, double* state_soa, float* v0, int32_t* elapsed, vo
     }
     if (err == hipSuccess) err = get_aux(e, v0, elapsed, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_get_state64");
+}
+
+int rr_counter_bits(const rr_env* e) { return e ? (int)e->kp.ep_shift : RR_EINVAL; }
+
+int rr_get_aux(rr_env* e, uint32_t* counter, float* ep_return, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_get_aux: null handle");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t err = hipSuccess;
+    if (counter) err = hipMemcpyAsync(counter, e->counter, sizeof(uint32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && ep_return)
+        err = hipMemcpyAsync(ep_return, e->ep_ret, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_get_aux");
+}
+
+int rr_set_aux(rr_env* e, const uint32_t* counter, const float* ep_return, void* stream)
+{
+    if (!e) return fail(RR_EINVAL, "rr_set_aux: null handle");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t err = hipSuccess;
+    if (counter) err = hipMemcpyAsync(e->counter, counter, sizeof(uint32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    if (err == hipSuccess && ep_return)
+        err = hipMemcpyAsync(e->ep_ret, ep_return, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_set_aux");
 }
 
 int rr_get_buffers(rr_env* e, rr_buffers* out)

@@ -404,7 +404,7 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
                vf_coef=0.5, max_grad_norm=0.5, generator=None, group=None):
     """SB3 1.6 PPO.train on the device-resident rollout (advantage normalisation per
     minibatch, clipped surrogate, unclipped value loss, entropy bonus, grad-norm clip).
-    ent_coef 0.01 as main_6DOF.py:114.
+    ent_coef 0.01 as main_6DOF.py:68.
 
     Multi-GPU (one policy replica per GPU): with a torch.distributed `group`
     every rank collects from its own env shard and updates on its own rollout; the

@@ -2,7 +2,7 @@
 
 Equivalent, for SB3's PPO, to ``DummyVecEnv([make_env] * N)`` with
 ``make_env`` = ``gym.make(id, **env_config)`` -> ``TimeLimit(max_episode_steps)``
--> ``Monitor`` (reference main_6DOF.py:64-70), but stepped by ONE launch of the
+-> ``Monitor`` (reference main_6DOF.py:18-24), but stepped by ONE launch of the
 fused HIP kernel for all N envs:
 
   * on-device auto-reset; ``infos[i]["terminal_observation"]`` holds the final

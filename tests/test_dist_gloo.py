@@ -32,39 +32,63 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_local, q):
+def _worker(rank, world, port, global_envs, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    _, off = shard(n_local * world, world, rank)
+    n_local, off = shard(global_envs, world, rank)
     gid = torch.arange(off, off + n_local, dtype=torch.float32)
-    obs = gid[:, None].repeat(1, 14) + torch.arange(14, dtype=torch.float32) * 1e-3
-    rew = -gid
-    done = (gid.long() % 3 == 0).to(torch.uint8)
-    g = ShardGather(n_local, 14, "cpu")
-    o, r, d = g(obs, rew, done)
-    q.put((rank, o.numpy().copy(), r.numpy().copy(), d.numpy().copy()))
+    g = ShardGather(n_local, 14, "cpu", global_envs=global_envs)
+    # the rows the step kernel writes (rr_step_rows): obs[14], reward, done 0 / 1
+    rows = g.local_rows
+    rows[:, :14] = gid[:, None] + torch.arange(14, dtype=torch.float32) * 1e-3
+    rows[:, 14] = -gid
+    rows[:, 15] = (gid.long() % 3 == 0).float()
+    o, r, d = g.gather()
+    res = [o.numpy().copy(), r.numpy().copy(), d.numpy().copy()]
+    # the legacy entry point: outputs produced elsewhere, copied into the send rows
+    o2, r2, d2 = g(rows[:, :14].clone() + 1, rows[:, 14].clone() - 1, (gid.long() % 2 == 0).to(torch.uint8))
+    res += [o2.numpy().copy(), r2.numpy().copy(), d2.numpy().copy()]
+    q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gather_world2_gloo():
-    world, n_local = 2, 6
+@pytest.mark.parametrize("global_envs", [12, 13])
+def test_gather_world2_gloo(global_envs):
+    """Equal (12 = 6 + 6) and padded uneven (13 = 7 + 6) shards reassemble in global env order."""
+    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_local, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, global_envs, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    gid = np.arange(world * n_local, dtype=np.float32)
-    for _, o, r, d in res:
+    gid = np.arange(global_envs, dtype=np.float32)
+    for _, (o, r, d, o2, r2, d2) in res:
+        assert o.shape == (global_envs, 14)
         np.testing.assert_array_equal(o[:, 0], gid)
+        np.testing.assert_array_equal(o[:, 13], gid + np.float32(13e-3))
         np.testing.assert_array_equal(r, -gid)
-        np.testing.assert_array_equal(d, (gid.astype(int) % 3 == 0).astype(np.uint8))
+        np.testing.assert_array_equal(d, (gid.astype(int) % 3 == 0).astype(np.float32))
+        np.testing.assert_array_equal(o2[:, 0], gid + 1)
+        np.testing.assert_array_equal(r2, -gid - 1)
+        np.testing.assert_array_equal(d2, (gid.astype(int) % 2 == 0).astype(np.float32))
+
+
+def test_gather_rejects_wrong_shard_size():
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        with pytest.raises(ValueError):
+            ShardGather(5, 14, "cpu", global_envs=6)
+    finally:
+        dist.destroy_process_group()
 
 
 class _FakeRollout:

@@ -1,0 +1,222 @@
+"""GPU: counter words, checkpoints, sharded stepping and the packed-row / all-gather path
+(the multi-GPU design of SURVEY.md §8e exercised on one GPU)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _env6():
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    return ENV_CONFIG_6DOF
+
+
+def _actions(n, na, steps, seed):
+    import torch
+
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(seed)
+    return [torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1 for _ in range(steps)]
+
+
+@pytest.mark.parametrize("model", [6, 3])
+def test_step_rows_is_bitwise_step(model):
+    """rr_step_rows writes (obs, reward, done) rows bitwise equal to rr_step's three outputs,
+    with the same state, truncation flags and reward terms, over steps with resets."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 4096 + 77
+    kw = _env6() if model == 6 else {}
+    a = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=30, compute_terms=True, **kw)
+    b = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=30, compute_terms=True, **kw)
+    a.reset()
+    b.reset()
+    rows = torch.empty((n, a.state_dim + 2), device="cuda:0")
+    ns = a.state_dim
+    for act in _actions(n, a.action_dim, 45, 3):
+        obs, rew, done, trunc = a.step(act)
+        b.step_rows(act, rows)
+        assert torch.equal(rows[:, :ns], obs)
+        assert torch.equal(rows[:, ns], rew)
+        assert torch.equal(rows[:, ns + 1], done.float())
+        assert torch.equal(b.truncated, trunc)
+        assert torch.equal(b.terms, a.terms)
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("model", [6, 3])
+def test_sharded_stepping_is_bitwise_one_batch(model):
+    """envs are independent and the reset stream is keyed on global ids, so three
+    uneven shards (rl_rocket_amd.dist.shard, env_id_offset = shard offset) step bitwise like one
+    batch of all envs: obs, rewards, done / truncated, terminal rows and state, over 60 steps
+    with TimeLimit 25 (every env resets at least twice)."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.dist import shard
+
+    n, world = 20000 + 3, 3
+    kw = _env6() if model == 6 else {}
+    whole = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=25, **kw)
+    parts = []
+    for r in range(world):
+        m, off = shard(n, world, r)
+        parts.append((off, m, RocketBatch(m, model=model, device="cuda:0", max_episode_steps=25, env_id_offset=off,
+                                          **kw)))
+    o_all = whole.reset()
+    for off, m, p in parts:
+        assert torch.equal(p.reset(), o_all[off:off + m])
+    resets = 0
+    for act in _actions(n, whole.action_dim, 60, 11):
+        obs, rew, done, trunc = whole.step(act)
+        idx, tobs, ret, ln = whole.fetch_done()
+        resets += len(idx)
+        for off, m, p in parts:
+            o2, r2, d2, t2 = p.step(act[off:off + m])
+            assert torch.equal(o2, obs[off:off + m])
+            assert torch.equal(r2, rew[off:off + m])
+            assert torch.equal(d2, done[off:off + m])
+            assert torch.equal(t2, trunc[off:off + m])
+            i2, to2, ret2, ln2 = p.fetch_done()
+            sel = (idx >= off) & (idx < off + m)
+            np.testing.assert_array_equal(i2 + off, idx[sel])
+            np.testing.assert_array_equal(to2, tobs[sel])
+            np.testing.assert_array_equal(ret2, ret[sel])
+            np.testing.assert_array_equal(ln2, ln[sel])
+    assert resets >= 2 * n
+    st = whole.get_state()
+    for off, m, p in parts:
+        st2 = p.get_state()
+        assert torch.equal(st2[0], st[0][:, off:off + m])
+        assert torch.equal(st2[1], st[1][off:off + m])
+        assert torch.equal(st2[2], st[2][off:off + m])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_graph_captured_step_and_allgather_rccl():
+    """The multi-GPU hot path on one GPU: rr_step_rows into ShardGather's send rows + ONE
+    RCCL all_gather_into_tensor ("nccl" backend, world 1), captured in a hipGraph. Replays give
+    bitwise the outputs of the same steps run eagerly through rr_step."""
+    import torch
+    import torch.distributed as dist
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.dist import ShardGather
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        n = 65536
+        a = RocketBatch(n, model=6, device=dev, max_episode_steps=30, **_env6())
+        b = RocketBatch(n, model=6, device=dev, max_episode_steps=30, **_env6())
+        a.reset()
+        b.reset()
+        g = ShardGather(n, 14, dev)
+        acts = _actions(n, 3, 8, 5)
+        g.step(b, acts[0])  # eager warm-up (communicator set up outside the capture)
+        a.step(acts[0])
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                for k in range(1, 4):
+                    g.step(b, acts[k])
+        torch.cuda.current_stream().wait_stream(s)
+        for rep in range(2):  # two replays = steps 1..3, 4..6 of the eager twin
+            graph.replay()
+            for k in range(1, 4):
+                obs, rew, done, _ = a.step(acts[k])
+            torch.cuda.synchronize()
+            assert torch.equal(g.obs, obs)
+            assert torch.equal(g.reward, rew)
+            assert torch.equal(g.done, done.float())
+        assert torch.equal(a.get_state()[0], b.get_state()[0])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_counter_layout_and_reset_keys_beyond_65536_episodes():
+    """The counter word holds the TimeLimit steps in E = bits(max_episode_steps) bits (10 for
+    the reference's TimeLimit 800) and the episode number above them (22 bits), so one env's
+    reset keys do not repeat after 65 536 episodes: episodes e and e + 65536 (and e + 2^21)
+    ending at the same step draw different initial conditions (with the round-1 16 / 16 layout
+    they were the same key)."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 64
+    b = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=800, **_env6())
+    assert b.counter_bits == 10
+    assert RocketBatch(8, model=6, device="cuda:0", max_episode_steps=0, **_env6()).counter_bits == 16
+    assert RocketBatch(8, model=6, device="cuda:0", max_episode_steps=1, **_env6()).counter_bits == 1
+    b.reset()
+    ck = b.checkpoint()
+    act = torch.zeros((n, 3), device="cuda:0")
+    ics = []
+    for ep in (5, 5 + 65536, 5 + (1 << 21)):
+        ck["counter"] = torch.as_tensor(b.make_counter(799, ep), device="cuda:0").expand(n).contiguous()
+        b.restore(ck)
+        obs, rew, done, trunc = b.step(act)  # step 800: TimeLimit -> reset keyed on (gid, counter word)
+        assert bool(trunc.all())
+        ics.append(obs.clone())
+        el, epn = b.split_counter(b.checkpoint()["counter"])
+        assert bool((el == 0).all()) and bool((epn == ep + 1).all())
+    for i in range(3):
+        for j in range(i + 1, 3):
+            assert not torch.equal(ics[i], ics[j])
+            assert bool((ics[i] != ics[j]).any(dim=1).all())  # every env's IC differs
+
+
+def test_checkpoint_restore_is_bitwise():
+    """checkpoint() / restore() round-trips state, v0, counter words (reset-stream keys) and
+    the Monitor running return: the steps after a restore are bitwise the steps after the
+    checkpoint, incl. the episode returns of finished episodes (set_state alone
+    dropped the running return and the episode field)."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 5000
+    b = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=40, **_env6())
+    b.reset()
+    acts = _actions(n, 3, 70, 9)
+    for act in acts[:30]:
+        b.step(act)
+    ck = {k: v.clone() for k, v in b.checkpoint().items()}
+
+    def run():
+        out = []
+        for act in acts[30:]:
+            obs, rew, done, trunc = b.step(act)
+            idx, tobs, ret, ln = b.fetch_done()
+            out.append((obs.clone(), rew.clone(), done.clone(), idx.copy(), ret.copy(), ln.copy()))
+        return out
+
+    first = run()
+    b.restore(ck)
+    second = run()
+    for x, y in zip(first, second):
+        for u, v in zip(x[:3], y[:3]):
+            assert torch.equal(u, v)
+        for u, v in zip(x[3:], y[3:]):
+            np.testing.assert_array_equal(u, v)
+    assert any(len(x[3]) for x in first)
+    # set_state without counter words keeps the episode field and clears the steps
+    cw = torch.as_tensor(b.make_counter(17, 123), device="cuda:0").expand(n).contiguous()
+    b.restore(dict(ck, counter=cw))
+    b.set_state(ck["state"], v0=ck["v0"])
+    el, ep = b.split_counter(b.checkpoint()["counter"])
+    assert bool((el == 0).all()) and bool((ep == 123).all())

@@ -1,10 +1,12 @@
-"""Kernel diagnostics on the GPU box: ablation builds (RR_DIAG) and an N sweep.
+"""Step-kernel N sweep on the GPU box (and the timing child of tools/ab_kernel.py).
 
-    python tools/diag_kernel.py [--ns 4096,65536,...] [--variants 0,1,2,3] [--model 6]
+    python tools/diag_kernel.py [--ns 4096,65536,...] [--model 6] [--lib path/to/librocket_hip.so]
 
-Each (variant, N) runs in its own child process (librocket_hip.so is loaded once per
-process; RR_LIB_PATH selects the build). Timing = HIP events around graph replays of
-64 back-to-back step launches on the launch stream.  Prints one JSON line per run.
+Each N runs in its own child process (librocket_hip.so is loaded once per process;
+RR_LIB_PATH selects the build). Timing = HIP events around graph replays of 64
+back-to-back step launches on the launch stream. Prints one JSON line per run. (The
+round-1 ablation builds, RR_DIAG, were removed from the product source in round 2; they
+live in the git history, DESIGN.md §3 keeps their numbers.)
 """
 import argparse
 import json
@@ -68,7 +70,7 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--ns", default="4096,16384,65536,262144,524288,1048576,4194304")
-    ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--lib", default=os.path.join(ROOT, "rl_rocket_amd", "librocket_hip.so"))
     ap.add_argument("--model", type=int, default=6)
     ap.add_argument("--integrator", default="rk4")
     ap.add_argument("--steps", type=int, default=2048)
@@ -76,24 +78,14 @@ def main():
     args = ap.parse_args()
     if args.child:
         return child(args)
-    from rl_rocket_amd import build as b
-
-    os.makedirs(args.out, exist_ok=True)
-    for v in args.variants.split(","):
-        lib = os.path.join(args.out, "librocket_hip_diag%s.so" % v)
-        cmd = b.command(out=lib, defines=("RR_DIAG=%s" % v[0],))
-        if v.endswith("slp"):  # A/B the SLP vectoriser
-            cmd = [c for c in cmd if c != "-fno-slp-vectorize"]
-        subprocess.check_call(cmd)
-        for n in [int(x) for x in args.ns.split(",")]:
-            env = dict(os.environ, RR_LIB_PATH=lib)
-            cmd = [sys.executable, __file__, "--child", "--tag", "diag%s" % v, "--n", str(n), "--model",
-                   str(args.model), "--integrator", args.integrator, "--steps", str(args.steps)]
-            r = subprocess.run(cmd, env=env, timeout=300)
-            if r.returncode != 0:
-                print(json.dumps({"variant": v, "n": n, "error": r.returncode}), flush=True)
-                if r.returncode < 0 or r.returncode > 1:
-                    sys.exit(r.returncode)
+    for n in [int(x) for x in args.ns.split(",")]:
+        env = dict(os.environ, RR_LIB_PATH=os.path.abspath(args.lib))
+        cmd = [sys.executable, __file__, "--child", "--tag", os.path.basename(args.lib), "--n", str(n), "--model",
+               str(args.model), "--integrator", args.integrator, "--steps", str(args.steps)]
+        r = subprocess.run(cmd, env=env, timeout=300)
+        if r.returncode != 0:
+            print(json.dumps({"n": n, "error": r.returncode}), flush=True)
+            sys.exit(r.returncode)
 
 
 if __name__ == "__main__":
