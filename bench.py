@@ -151,8 +151,9 @@ def host_cores():
 def cpu_baseline(model, seconds, seed=0, nthreads=1, n=1024):
     """The CPU oracle (faithful scipy-RK45 restatement in C) stepping a bounded sample of
     the same workload: envs from the same init_space, U(-1,1) actions, auto-reset on done,
-    TimeLimit 800; `nthreads` OpenMP threads over the env batch (SURVEY.md §8d baselines
-    (i) 1 core and (ii) all host cores)."""
+    TimeLimit 800. n = 1: ONE env per call from a Python loop, the shape of the reference's
+    single-env ``Rocket6DOF.step()`` (rocket_env.py:690, 150); n > 1: the batched port,
+    `nthreads` OpenMP threads over the env batch (SURVEY.md §8d baselines (i) and (ii))."""
     import numpy as np
 
     from oracle import oracle as O
@@ -161,8 +162,6 @@ def cpu_baseline(model, seconds, seed=0, nthreads=1, n=1024):
     cfg = O.make_cfg(model, **kw)
     ns = 14 if model == 6 else 7
     na = 3 if model == 6 else 2
-    if model == 6:
-        _, lo, hi, _, _ = O.derived6(**kw)
     lo_ic = (np.float32(kw["IC"]) - np.float32(kw["ICRange"]) / 2).astype(np.float32)
     hi_ic = (np.float32(kw["IC"]) + np.float32(kw["ICRange"]) / 2).astype(np.float32)
     rng = np.random.default_rng(seed)
@@ -195,24 +194,55 @@ def cpu_baseline(model, seconds, seed=0, nthreads=1, n=1024):
             s[d] = ic[d]
             el[d] = 0
             t[d] = 0
+    name = "6DOF" if model == 6 else "3DOF"
+    if n == 1:
+        what = ("%d env-steps of ONE %s env, one oracle call per step from a Python loop (the shape of the "
+                "reference's single-env step(), rocket_env.py:%d), env_config ICs, U(-1,1) actions, auto-reset, "
+                "TimeLimit 800" % (steps, name, 690 if model == 6 else 150))
+    else:
+        what = ("%d env-steps of %s (%d envs x %d steps per call, batched oracle ro_step_batch), env_config ICs, "
+                "U(-1,1) actions, auto-reset, TimeLimit 800" % (steps, name, n, steps // n))
     return {"value": steps / busy, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
-            "sample": "%d env-steps of %s (%d envs x %d steps, env_config ICs, U(-1,1) actions, auto-reset, "
-                      "TimeLimit 800) through oracle/librocket_oracle.so ro_step_batch, %d thread(s); "
-                      "reference Python step() measured 569 (6DOF) / 3396 (3DOF) steps/s/core in the survey "
-                      "container (BASELINE.md)" % (steps, "6DOF" if model == 6 else "3DOF", n, steps // n, nthreads)}
+            "sample": what + ", %d thread(s), oracle/librocket_oracle.so (scipy RK45 + brentq restated in C)" % nthreads}
+
+
+def cpu_baselines(model, seconds, cores):
+    """cpu_baseline block of the bench line: the single-env leg (the north star's 'reference
+    single-env CPU step()'), the batched port on 1 core and on all host cores, the 3DOF single
+    env of configs[0], and the reference's own Python step() rates measured in the survey
+    container (it cannot run on the GPU box)."""
+    head = cpu_baseline(model, seconds * 0.35, n=1)
+    head["batched_1core"] = cpu_baseline(model, seconds * 0.25)
+    if cores > 1:
+        head["all_cores"] = cpu_baseline(model, seconds * 0.2, nthreads=cores, n=8192)
+    if model == 6:
+        head["configs0_3dof_single_env"] = cpu_baseline(3, seconds * 0.2, n=1)
+    head["reference_python_step_survey"] = {"6DOF": 569, "3DOF": 3396, "unit": "env-steps/s", "cores": 1,
+                                            "source": "reference Rocket6DOF / Rocket step(), measured in the survey "
+                                                      "container (SURVEY.md §6, BASELINE.md), not on this box"}
+    return head
 
 
 def stored_traffic(model, n):
     """Per-launch HBM bytes of the same kernel/config from the latest committed rocprofv3 PMC
-    passes (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or (None, None)."""
+    passes (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), only if they were measured on
+    THIS kernel code (same rl_rocket_amd.build.source_hash); else (None, reason)."""
     import glob
 
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_n%d.json" % n)))
+    from rl_rocket_amd.build import source_hash
+
+    want = source_hash()
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "pmc_traffic_n%d.json" % n), recursive=True),
+                  key=os.path.getmtime)
+    stale = None
     for path in reversed(hits):
         d = json.load(open(path))
-        if d.get("kernel", "").startswith("step_kernel<%d," % model):
+        if not d.get("kernel", "").startswith("step_kernel<%d," % model):
+            continue
+        if d.get("source_hash") == want:
             return d["traffic_bytes"], os.path.relpath(path, ROOT)
-    return None, None
+        stale = stale or os.path.relpath(path, ROOT)
+    return None, ("no PMC traffic file for kernel source %s (latest, other source: %s)" % (want, stale))
 
 
 def main():
@@ -379,12 +409,7 @@ def main():
                      "bytes_per_env_step": BYTES_PER_STEP[model]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(model, args.cpu_seconds)
-        c = host_cores()
-        if c > 1:  # SURVEY.md §8d baseline (ii): the batched oracle on all host cores
-            result["cpu_baseline"]["all_cores"] = {
-                k: v for k, v in cpu_baseline(model, max(2.0, args.cpu_seconds / 3), nthreads=c, n=8192).items()
-                if k in ("value", "unit", "cores", "sample")}
+        result["cpu_baseline"] = cpu_baselines(model, args.cpu_seconds, host_cores())
     env.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

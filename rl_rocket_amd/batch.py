@@ -79,21 +79,33 @@ class RocketBatch:
     def seed(self, seed):
         _lib.check(self.lib.rr_seed(self._h, int(seed) & (2 ** 64 - 1), self._stream()), "rr_seed")
 
-    def reset(self, mask=None):
+    def reset(self, mask=None, obs=None):
+        """Fresh initial conditions for the envs where mask != 0 (all when None); writes the
+        obs of every env into `obs` (default: the env's own obs tensor) and returns it."""
         m = None
         if mask is not None:
             m = self.torch.as_tensor(mask, device=self.device).to(self.torch.uint8).contiguous()
-        _lib.check(self.lib.rr_reset(self._h, _ptr(m), _ptr(self.obs), self._stream()), "rr_reset")
-        return self.obs
+        obs = self.obs if obs is None else obs
+        _lib.check(self.lib.rr_reset(self._h, _ptr(m), _ptr(obs), self._stream()), "rr_reset")
+        return obs
 
-    def step(self, action):
-        """One env step for all envs. Returns the (reused) output tensors
-        (obs [N,ns], reward [N], done [N] u8, truncated [N] u8)."""
+    def alloc_outputs(self):
+        """A fresh set of step output tensors (obs, reward, done, truncated) for step(out=...)."""
+        t = self.torch
+        n, ns = self.num_envs, self.state_dim
+        return (t.empty((n, ns), dtype=t.float32, device=self.device), t.empty((n,), dtype=t.float32, device=self.device),
+                t.empty((n,), dtype=t.uint8, device=self.device), t.empty((n,), dtype=t.uint8, device=self.device))
+
+    def step(self, action, out=None):
+        """One env step for all envs. Returns the output tensors (obs [N,ns], reward [N], done
+        [N] u8, truncated [N] u8): the env's own, reused by every step, or the set `out`
+        (alloc_outputs(); e.g. double-buffered outputs that stay valid for one more step)."""
         action = self._check_action(action)
         self._last_action = action  # keep alive until the kernel has run
-        _lib.check(self.lib.rr_step(self._h, _ptr(action), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
-                                    _ptr(self.truncated), _ptr(self.terms), self._stream()), "rr_step")
-        return self.obs, self.reward, self.done, self.truncated
+        obs, rew, done, trunc = out if out is not None else (self.obs, self.reward, self.done, self.truncated)
+        _lib.check(self.lib.rr_step(self._h, _ptr(action), _ptr(obs), _ptr(rew), _ptr(done), _ptr(trunc),
+                                    _ptr(self.terms), self._stream()), "rr_step")
+        return obs, rew, done, trunc
 
     def step_rows(self, action, rows):
         """One env step writing obs, reward and done as rows [N, state_dim + 2] fp32 (obs,

@@ -41,6 +41,20 @@ def command(resource_usage=False, out=OUT, defines=(), extra=()):
     return cmd
 
 
+def source_hash():
+    """sha256 of everything that determines the kernels' code: the HIP sources, the C-ABI
+    header and the compile command (tools/pmc_traffic.py stamps its output with it; bench.py
+    only quotes a PMC traffic file measured on the same kernel code)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for path in [SRC, HEADER] + DEPS:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(command()[1:-1]).replace(ROOT, "").encode())
+    return h.hexdigest()[:16]
+
+
 def up_to_date():
     if not os.path.exists(OUT):
         return False

@@ -292,7 +292,10 @@ class DeviceRollout:
             nobs, rew, done, trunc = env.step(self._clipped)
             # SB3 1.6: bootstrap timeouts with the value of the terminal observation
             env.copy_terminal(out=(self._tobs, None, None))
-            torch.addcmul(rew, pol.value(self._tobs), trunc.float(), value=self.gamma, out=self._r)
+            # a select, as the fused kernels: terminal rows of envs that are not done are stale
+            # (possibly non-finite), and NaN * 0 would leak into the reward
+            torch.where(trunc.bool(), torch.addcmul(rew, pol.value(self._tobs), trunc.float(), value=self.gamma),
+                        rew, out=self._r)
             self.rewards[t].copy_(self._r)
             self.last_obs.copy_(nobs)
             self.last_start.copy_(done.float())

@@ -14,7 +14,13 @@ fused HIP kernel for all N envs:
     host cost per step is O(#done), not O(N) dict building.
 
 ``device_outputs=True`` returns torch tensors that stay in HBM (no host copy);
-otherwise numpy arrays as SB3 expects.
+otherwise numpy arrays as SB3 expects. Device outputs are double-buffered: the tensors
+returned by step t (and reset) stay unchanged through step t + 1 and are overwritten by
+step t + 2 — what SB3's collect_rollouts needs (it stores ``_last_obs`` from step t after
+stepping t + 1). Their ``infos`` are built lazily from a per-step device snapshot (done /
+truncated flags and terminal rows of THAT step), so reading them late still describes their
+own step; infos nobody reads are built before their snapshot is reused, so every finished
+episode reaches the Monitor statistics, in step order.
 """
 import time
 from collections.abc import Sequence
@@ -68,6 +74,44 @@ class LazyInfos(Sequence):
         return sorted(k for k, v in self._done.items() if "terminal_observation" in v)
 
 
+class _DeviceInfos(LazyInfos):
+    """infos of one device-output step, built on first access (or before the step's snapshot
+    is reused) from that step's own done / truncated flags and terminal rows."""
+
+    def __init__(self, venv, slot):
+        super().__init__(venv.num_envs, None)
+        self._venv, self._slot = venv, slot
+        self._built = None
+
+    def _build(self):
+        if self._built is None:
+            v = self._venv
+            while v._pending and v._pending[0] is not self:  # earlier steps first (Monitor order)
+                v._pending[0]._build()
+            _, _, done, trunc = self._slot["out"]
+            done_h = done.cpu().numpy().astype(bool)
+            done_info = {}
+            if done_h.any():
+                idx = np.nonzero(done_h)[0]
+                ii = v.batch.torch.as_tensor(idx, device=v.batch.device)
+                tobs, ret, ln = (x.index_select(0, ii).cpu().numpy() for x in self._slot["term"])
+                done_info = v._done_dicts(idx, tobs, ret, ln, trunc.cpu().numpy())
+            self._built = v._finish_infos(done_info, self._slot["terms"])
+            if v._pending and v._pending[0] is self:
+                v._pending.pop(0)
+            self._slot["infos"] = None
+        return self._built
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        return self._build()[i]
+
+    def done_indices(self):
+        return self._build().done_indices()
+
+
 class RocketVecEnv(_VecEnvBase):
     metadata = {"render.modes": []}
 
@@ -95,78 +139,102 @@ class RocketVecEnv(_VecEnvBase):
         self.total_steps = 0
         self.cfg = self.batch.cfg
         self.state_names = self.batch.cfg.state_names if hasattr(self.batch.cfg, "state_names") else None
+        if device_outputs:
+            self._init_device_sets()
 
     # -- VecEnv API ------------------------------------------------------------------------------------------
     def reset(self):
+        if self.device_outputs:
+            self._flush_all()
+            self._slot = 0
+            return self.batch.reset(obs=self._sets[0]["out"][0])
         obs = self.batch.reset()
-        return obs if self.device_outputs else obs.cpu().numpy()
+        return obs.cpu().numpy()
 
     def step_async(self, actions):
         self._actions = actions
 
     def step_wait(self):
-        obs, rew, done, trunc = self.batch.step(self._actions)
         self.total_steps += self.num_envs
         if self.device_outputs:
-            return obs, rew, done.bool(), self._lazy_infos_device(done, trunc)
+            return self._step_device()
+        obs, rew, done, trunc = self.batch.step(self._actions)
         obs_h = obs.cpu().numpy()
         rew_h = rew.cpu().numpy()
         done_h = done.cpu().numpy().astype(bool)
-        infos = self._infos_from_host(done_h, trunc)
-        return obs_h, rew_h, done_h, infos
+        done_info = {}
+        if done_h.any():
+            idx, tobs, ret, ln = self.batch.fetch_done()
+            done_info = self._done_dicts(idx, tobs, ret, ln, trunc.cpu().numpy())
+        return obs_h, rew_h, done_h, self._finish_infos(done_info, self.batch.terms)
 
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
 
-    def _infos_from_host(self, done_h, trunc):
+    def _done_dicts(self, idx, tobs, ret, ln, trunc_h):
+        """infos of the done envs (SB3 DummyVecEnv + TimeLimit + Monitor), Monitor stats recorded."""
         done_info = {}
-        if done_h.any():
-            idx, tobs, ret, ln = self.batch.fetch_done()
-            trunc_h = trunc.cpu().numpy()
-            now = round(time.time() - self._t_start, 6)
-            for k, i in enumerate(idx.tolist()):
-                d = {"terminal_observation": tobs[k].copy()}
-                if trunc_h[i]:
-                    d["TimeLimit.truncated"] = True
-                elif self.max_episode_steps and ln[k] >= self.max_episode_steps:
-                    d["TimeLimit.truncated"] = False
-                if self.monitor:
-                    d["episode"] = {"r": round(float(ret[k]), 6), "l": int(ln[k]), "t": now}
-                    self.episode_returns.append(float(ret[k]))
-                    self.episode_lengths.append(int(ln[k]))
-                    self.episode_times.append(now)
-                done_info[i] = d
-        terms = self.batch.terms.cpu().numpy() if self.info_terms else None
+        now = round(time.time() - self._t_start, 6)
+        for k, i in enumerate(np.asarray(idx).tolist()):
+            d = {"terminal_observation": np.asarray(tobs[k]).copy()}
+            if trunc_h[i]:
+                d["TimeLimit.truncated"] = True
+            elif self.max_episode_steps and ln[k] >= self.max_episode_steps:
+                d["TimeLimit.truncated"] = False
+            if self.monitor:
+                d["episode"] = {"r": round(float(ret[k]), 6), "l": int(ln[k]), "t": now}
+                self.episode_returns.append(float(ret[k]))
+                self.episode_lengths.append(int(ln[k]))
+                self.episode_times.append(now)
+            done_info[i] = d
+        return done_info
+
+    def _finish_infos(self, done_info, terms_dev):
+        terms = terms_dev.cpu().numpy() if self.info_terms else None
         if terms is not None:
             for i, d in done_info.items():
                 LazyInfos._fill_terms(LazyInfos(0, {}, terms, self.cfg.term_names), i, d)
         return LazyInfos(self.num_envs, done_info, terms, self.cfg.term_names)
 
-    def _lazy_infos_device(self, done, trunc):
-        batch = self
+    # -- device outputs: double-buffered step outputs + per-step snapshots for the lazy infos ---------------
+    def _init_device_sets(self):
+        t = self.batch.torch
+        n, ns, dev = self.num_envs, self.batch.state_dim, self.batch.device
+        self._sets = []
+        for _ in range(2):
+            self._sets.append({
+                "out": self.batch.alloc_outputs(),
+                "term": (t.empty((n, ns), dtype=t.float32, device=dev), t.empty((n,), dtype=t.float32, device=dev),
+                         t.empty((n,), dtype=t.int32, device=dev)),
+                "terms": None if self.batch.terms is None else t.empty_like(self.batch.terms),
+                "infos": None,
+            })
+        self._slot = 0
+        self._pending = []  # unbuilt _DeviceInfos in step order
 
-        class _DeviceInfos(LazyInfos):
-            def __init__(self):
-                super().__init__(batch.num_envs, None)
-                self._built = None
+    def _flush_all(self):
+        while self._pending:
+            self._pending[0]._build()
 
-            def _build(self):
-                if self._built is None:
-                    self._built = batch._infos_from_host(done.cpu().numpy().astype(bool), trunc)
-                return self._built
-
-            def __getitem__(self, i):
-                return self._build()[i]
-
-            def done_indices(self):
-                return self._build().done_indices()
-
-        return _DeviceInfos()
+    def _step_device(self):
+        self._slot ^= 1
+        st = self._sets[self._slot]
+        if st["infos"] is not None:  # its snapshot is about to be reused: build it first
+            st["infos"]._build()
+        obs, rew, done, trunc = self.batch.step(self._actions, out=st["out"])
+        self.batch.copy_terminal(out=st["term"])  # this step's terminal rows, device to device
+        if st["terms"] is not None:
+            st["terms"].copy_(self.batch.terms)
+        infos = _DeviceInfos(self, st)
+        st["infos"] = infos
+        self._pending.append(infos)
+        return obs, rew, done.bool(), infos
 
     def close(self):
+        if self.device_outputs and getattr(self, "_pending", None):
+            self._flush_all()
         self.batch.close()
-
     def seed(self, seed=None):
         if seed is None:
             seed = int(np.random.randint(0, 2 ** 31 - 1))

@@ -39,65 +39,155 @@ def test_rocket6dof_shim_reset_and_step(golden6, oracle_mod):
     env.close()
 
 
-def test_rocket3dof_shim(golden3):
+def test_rocket3dof_shim(golden3, oracle_mod):
+    """The 3DOF single-env shim: the reference's reset stream, float64 obs, and step values
+    (state, obs, reward, every reward term, done) against the oracle on the same IC / action."""
     from rl_rocket_amd.envs import Rocket
 
     env = Rocket()
     obs = env.reset()
     assert obs.dtype == np.float64 and obs.shape == (7,)  # the reference's 3DOF obs is float64
-    np.testing.assert_array_equal(env.SIM.states[0], golden3["resets_seed42"][0])
-    obs, reward, done, info = env.step(np.float32([0.1, 0.3]))
-    assert "attitude_hint" in info["rewards_dict"]
+    ic = golden3["resets_seed42"][0]
+    np.testing.assert_array_equal(env.SIM.states[0], ic)
+    a = np.float32([0.1, 0.3])
+    obs, reward, done, info = env.step(a)
+    assert isinstance(reward, float) and isinstance(done, bool)
+    assert set(info["rewards_dict"]) == {"velocity_tracking", "thrust_penalty", "eta", "attitude_constraint",
+                                         "attitude_hint", "rew_goal"}
+    cfg = oracle_mod.make_cfg(3, **oracle_mod.DEFAULTS_3DOF)
+    ref = oracle_mod.step(cfg, ic[None], 0.0, ic[None].astype(np.float64), a[None])
+    norm = cfg.normalizer[:7]
+    assert oracle_mod.floored_rel(env.SIM.states[-1], ref["state_out"][0], norm).max() < 1e-5
+    assert oracle_mod.floored_rel(obs, ref["obs"][0], 1.0).max() < 1e-5
+    assert abs(reward - ref["reward"][0]) < 1e-5 * max(1, abs(ref["reward"][0]))
+    for j, k in enumerate(["velocity_tracking", "thrust_penalty", "eta", "attitude_constraint", "attitude_hint",
+                           "rew_goal"]):
+        assert abs(info["rewards_dict"][k] - ref["terms"][0][j]) < 1e-5 * max(1, abs(ref["terms"][0][j])), k
+    assert done == bool(ref["done"][0])
     env.close()
 
 
 def test_vec_env_sb3_semantics():
+    """DummyVecEnv + TimeLimit(50) + Monitor semantics, against independently stepped values:
+    a twin RocketBatch WITHOUT auto-reset, restored before every step to the vec env's own
+    pre-step checkpoint, steps the same actions — its obs are the vec env's obs for running
+    envs and info["terminal_observation"] for done ones, its rewards and done flags are the
+    vec env's. Monitor's episode r / l equal the host sums of the returned rewards and the
+    step counts; TimeLimit truncates exactly at 50 steps (random-action episodes end by the
+    ground or the bounds after 44-105 steps, SURVEY.md §6, so both kinds of ends occur)."""
+    from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
     from rl_rocket_amd.vec_env import RocketVecEnv
 
-    n = 4096
-    env = RocketVecEnv(n, model="6DOF", device="cuda:0", max_episode_steps=5, monitor=True, **ENV_CONFIG_6DOF)
+    n, L = 4096, 50
+    env = RocketVecEnv(n, model="6DOF", device="cuda:0", max_episode_steps=L, monitor=True, **ENV_CONFIG_6DOF)
+    twin = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=L, auto_reset=False, **ENV_CONFIG_6DOF)
     obs = env.reset()
     assert obs.shape == (n, 14) and obs.dtype == np.float32
     rng = np.random.default_rng(0)
-    seen_trunc = False
-    for k in range(12):
-        obs, rew, done, infos = env.step(rng.uniform(-1, 1, (n, 3)).astype(np.float32))
+    ep_ret = np.zeros(n, np.float64)
+    ep_len = np.zeros(n, np.int64)
+    seen_trunc = seen_term = 0
+    for k in range(120):
+        a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+        twin.restore(env.batch.checkpoint())
+        t_obs, t_rew, t_done, t_trunc = (x.cpu().numpy() for x in twin.step(a))
+        obs, rew, done, infos = env.step(a)
         assert rew.shape == (n,) and done.dtype == bool and len(infos) == n
+        np.testing.assert_array_equal(rew, t_rew)
+        np.testing.assert_array_equal(done, t_done.astype(bool))
+        np.testing.assert_array_equal(obs[~done], t_obs[~done])
+        ep_ret += rew
+        ep_len += 1
         idx = np.nonzero(done)[0]
         assert infos.done_indices() == idx.tolist()
-        for i in idx[:50]:
+        assert (ep_len[idx] <= L).all() and (done[ep_len == L]).all()  # TimeLimit(L): done at the latest at L
+        for i in idx[:200]:
             d = infos[i]
-            assert d["terminal_observation"].shape == (14,)
-            assert "episode" in d and d["episode"]["l"] <= 5
+            np.testing.assert_array_equal(d["terminal_observation"], t_obs[i])
+            assert d["episode"]["l"] == ep_len[i]
+            assert abs(d["episode"]["r"] - ep_ret[i]) <= 1e-5 * max(1.0, abs(ep_ret[i]))
             if d.get("TimeLimit.truncated"):
-                seen_trunc = True
-                assert d["episode"]["l"] == 5
-        if k == 4:  # every env has either ended before or hits the limit now
-            assert done.all() or env.episode_lengths
-    assert seen_trunc
-    assert np.all(np.abs(obs) < 10)
+                seen_trunc += 1
+                assert ep_len[i] == L and t_trunc[i]
+            else:
+                seen_term += 1
+                assert not t_trunc[i]
+        for i in np.nonzero(~done)[0][:50]:
+            assert infos[i] == {}
+        ep_ret[idx] = 0
+        ep_len[idx] = 0
+    assert seen_trunc and seen_term
+    assert env.episode_lengths and len(env.episode_lengths) == len(env.episode_returns)
     env.close()
+    twin.close()
 
 
-def test_reward_annealing_flag():
-    """RR_FLAG_REWARD_ANNEALING == RewardAnnealing (wrappers.py:72-86) on the kernel's own terms."""
+def test_vec_env_device_outputs_double_buffered():
+    """device_outputs=True (ADVICE r1): the tensors of step t are unchanged after step t + 1;
+    infos read late (after later steps) describe their own step, infos never read still reach
+    the Monitor statistics — all equal to a host-output vec env stepping the same actions."""
     import torch
-    from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.vec_env import RocketVecEnv
 
-    n = 8192
-    b = RocketBatch(n, model=6, device="cuda:0", reward_annealing=True, compute_terms=True, **ENV_CONFIG_6DOF)
-    b.reset()
-    g = torch.Generator(device="cuda:0")
-    g.manual_seed(5)
-    for _ in range(30):
-        a = torch.rand((n, 3), device="cuda:0", generator=g) * 2 - 1
-        _, rew, _, _ = b.step(a)
-        t = b.terms
-        ref = t[3] + t[4] - 0.004 * (a[:, 2] + 1)
-        torch.testing.assert_close(rew, ref, rtol=1e-6, atol=1e-6)
-    b.close()
+    n = 2048
+    dev = RocketVecEnv(n, model="6DOF", device="cuda:0", max_episode_steps=6, device_outputs=True, **ENV_CONFIG_6DOF)
+    host = RocketVecEnv(n, model="6DOF", device="cuda:0", max_episode_steps=6, **ENV_CONFIG_6DOF)
+    o_d, o_h = dev.reset(), host.reset()
+    np.testing.assert_array_equal(o_d.cpu().numpy(), o_h)
+    rng = np.random.default_rng(1)
+    held, kept_infos, host_infos = [], [], []
+    for k in range(20):
+        a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+        od, rd, dd, idv = dev.step(torch.from_numpy(a).cuda())
+        oh, rh, dh, ih = host.step(a)
+        snap = (od.clone(), rd.clone(), dd.clone())
+        if held:  # the previous step's tensors survived this step
+            for x, y in zip(held[-1][0], held[-1][1]):
+                assert torch.equal(x, y)
+        held.append((snap, (od, rd, dd)))
+        np.testing.assert_array_equal(od.cpu().numpy(), oh)
+        np.testing.assert_array_equal(rd.cpu().numpy(), rh)
+        np.testing.assert_array_equal(dd.cpu().numpy(), dh)
+        if k % 3 == 0:
+            kept_infos.append(idv)  # read after later steps
+            host_infos.append(ih)
+    for idv, ih in zip(kept_infos, host_infos):
+        assert idv.done_indices() == ih.done_indices()
+        for i in ih.done_indices():
+            np.testing.assert_array_equal(idv[i]["terminal_observation"], ih[i]["terminal_observation"])
+            assert idv[i]["episode"]["l"] == ih[i]["episode"]["l"]
+            assert idv[i]["episode"]["r"] == ih[i]["episode"]["r"]
+    dev.close()
+    assert dev.episode_lengths == host.episode_lengths  # every step's infos built, in step order
+    assert dev.episode_returns == host.episode_returns
+    host.close()
+
+
+@pytest.mark.parametrize("model", [6, 3])
+def test_reward_annealing_flag_vs_reference_terms(model, golden6, golden3):
+    """RR_FLAG_REWARD_ANNEALING against the reference's formula (wrappers.py:68-86:
+    attitude_constraint + rew_goal - xi * (thrust action + 1), no bounds penalty) evaluated on
+    the REFERENCE's own reward terms of the golden rows (not the kernel's terms)."""
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from gpu_util import TOL_REWARD, run_rows
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF, make_config
+
+    g = golden6 if model == 6 else golden3
+    kw = ENV_CONFIG_6DOF if model == 6 else {}
+    xi = make_config(model, **kw).kwargs["reward_coeff"]["xi"]
+    out = run_rows(model, g, reward_annealing=True, **kw)
+    names = make_config(model, **kw).term_names
+    att, goal = names.index("attitude_constraint"), names.index("rew_goal")
+    a_t = g["action"][:, 2 if model == 6 else 1].astype(np.float64)
+    ref = g["terms"][:, att] + g["terms"][:, goal] - xi * (a_t + 1.0)
+    err = np.abs(out["reward"] - ref) / np.maximum(np.abs(ref), 1.0)
+    assert err.max() < TOL_REWARD, err.max()
+    assert (np.abs(g["terms"][:, att]) > 0).any()  # the attitude term is exercised by the golden rows
+    if model == 6:
+        assert (g["terms"][:, goal] > 0).any()     # and the landing bonus (G3 rows)
 
 
 def test_euler_mode_is_declared_non_parity(golden3):
@@ -234,3 +324,42 @@ def test_gym_vector_surface():
     assert len(infos) == n and all("terminal_observation" in infos[i] for i in range(0, n, 97))
     assert all(infos[i]["TimeLimit.truncated"] in (True, False) for i in range(0, n, 97))
     env.close()
+
+
+def test_sb3_check_env_on_shims():
+    """SB3 1.6 check_env's assertions (restated in tests/sb3_check.py) on the drop-in
+    Rocket6DOF, as the reference's test_6DOF_sb_integration.py:15-18 runs them, except the
+    render check (rendering — pyvista / pygame — is out of scope; render() raises). 3DOF: the reference's
+    Rocket returns float64 obs (rocket_env.py:175) against a float32 Box, which gym 0.21's
+    Box.contains rejects (can_cast float64 -> float32 is False) — a reference quirk the shim
+    reproduces; every other check passes on the obs cast to float32."""
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from sb3_check import check_env
+    from rl_rocket_amd.envs import Rocket, Rocket6DOF
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+
+    env = Rocket6DOF(**ENV_CONFIG_6DOF)
+    warns = check_env(env, skip_render_check=True)
+    assert warns == []
+    env.close()
+
+    env3 = Rocket()
+    obs = env3.reset()
+    assert obs.dtype == np.float64 and not env3.observation_space.contains(obs)
+    assert env3.observation_space.contains(obs.astype(np.float32))
+
+    class _F32:  # the same env seen through a float32 obs cast
+        def __init__(self, e):
+            self.e, self.observation_space, self.action_space, self.metadata = e, e.observation_space, \
+                e.action_space, e.metadata
+
+        def reset(self):
+            return self.e.reset().astype(np.float32)
+
+        def step(self, a):
+            o, r, d, i = self.e.step(a)
+            return o.astype(np.float32), r, d, i
+
+    assert check_env(_F32(env3)) == []
+    env3.close()

@@ -291,3 +291,69 @@ def test_one_launch_rollout_bitwise_equals_two_launch(model, prec, collect_nt, m
     assert a.starts[1:].sum() > 0 and (a.rewards != 0).any()
     for ro in ros:
         ro.env.close()
+
+
+def test_rollout_collect_full_size_configs4():
+    """BASELINE configs[4] at its size: N = 65536 6DOF envs, TimeLimit 800, n_steps 16 (the
+    bench's collect), fp32 policy. The one-launch collect (rr_rollout_collect) is bitwise the
+    per-step path (rr_rollout_step launches, main_6DOF.py:62-69 scale-up); its values and
+    action means match the fp32 PyTorch MlpPolicy on the collected obs, and its log-probs are
+    the PyTorch log-density of the stored actions under that policy."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout
+
+    n, T = 65536, 16
+    pol = _policy(14, 3, seed=4)
+    ros = []
+    for per_step in (False, True):
+        env = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=800, **ENV_CONFIG_6DOF)
+        ros.append(DeviceRollout(env, pol, n_steps=T, policy_dtype="fp32", one_launch=True, per_step=per_step,
+                                 seed=21))
+    for _ in range(2):
+        for ro in ros:
+            ro.collect()
+    torch.cuda.synchronize()
+    a, b = ros
+    for name in ("obs", "actions", "values", "log_probs", "starts", "rewards", "advantages", "returns",
+                 "last_value", "last_done"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    for x, y in zip(a.env.get_state(), b.env.get_state()):
+        assert torch.equal(x, y)
+    with torch.no_grad():
+        mean, value = pol(a.obs.reshape(-1, 14))
+        lp = pol.log_prob(mean, a.actions.reshape(-1, 3))
+    assert (a.values.reshape(-1) - value).abs().max().item() < TOL
+    assert (a.log_probs.reshape(-1) - lp).abs().max().item() < 5e-4
+    # the stored actions are mean + std * N(0, 1) noise around the PyTorch means
+    z = ((a.actions.reshape(-1, 3) - mean) / pol.log_std.exp()).double()
+    assert abs(z.mean().item()) < 0.01 and abs(z.std().item() - 1.0) < 0.01
+    assert a.starts[1:].sum() > 0 and torch.isfinite(a.advantages).all()
+    for ro in ros:
+        ro.env.close()
+
+
+def test_unfused_bootstrap_ignores_stale_terminal_rows():
+    """the PyTorch rollout path selects r + gamma V(terminal obs) only where an env
+    was truncated, so a NaN left in the terminal buffer of a running env cannot reach its reward."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout
+
+    n = 2048
+    env = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=5, **ENV_CONFIG_6DOF)
+    ro = DeviceRollout(env, _policy(14, 3, seed=6), n_steps=8, fused=False)
+    env.copy_terminal()  # warm
+    orig = env.copy_terminal
+
+    def poisoned(out=None):  # every terminal row NaN except where the last step truncated
+        res = orig(out)
+        res[0][env.truncated == 0] = float("nan")
+        return res
+
+    env.copy_terminal = poisoned
+    ro.collect()
+    assert torch.isfinite(ro.rewards).all() and torch.isfinite(ro.advantages).all()
+    env.close()

@@ -5,17 +5,6 @@ import numpy as np
 from rl_rocket_amd.vec_env import LazyInfos, RocketVecEnv
 
 
-class _T:
-    def __init__(self, a):
-        self.a = np.asarray(a)
-
-    def cpu(self):
-        return self
-
-    def numpy(self):
-        return self.a
-
-
 class _FakeBatch:
     def __init__(self, n):
         self.num_envs = n
@@ -46,9 +35,9 @@ def _env(n=5):
 
 def test_done_infos_match_sb3_semantics():
     env = _env()
-    done = np.array([False, True, False, True, False])
-    trunc = _T(np.array([0, 1, 0, 0, 0], np.uint8))
-    infos = env._infos_from_host(done, trunc)
+    trunc = np.array([0, 1, 0, 0, 0], np.uint8)
+    idx, tobs, ret, ln = env.batch.fetch_done()
+    infos = env._finish_infos(env._done_dicts(idx, tobs, ret, ln, trunc), None)
     assert len(infos) == 5
     assert infos[0] == {} and infos[2] == {} and infos[4] == {}
     assert infos[1]["TimeLimit.truncated"] is True

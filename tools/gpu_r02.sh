@@ -12,7 +12,7 @@ OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 step() {  # step NAME TIMEOUT cmd...: 0 = ok, 1 = test failures (continue), anything else = stop
   local name=$1 to=$2; shift 2
-  echo "[$name] start $(date +%T)"
+  echo "[$name] start $(date +%T)" >&2
   timeout -k 10 "$to" "$@"
   local rc=$?
   echo "[$name] exit $rc" | tee -a "$OUT/status.txt"
@@ -40,6 +40,18 @@ if [ "${PMC:-1}" = 1 ]; then
   step pmc_GRBM 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmc_GRBM" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $BENCH_ARGS > "$OUT/pmc_GRBM.log" 2>&1
   for C in FETCH_SIZE WRITE_SIZE; do
     step pmc_$C 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $BENCH_ARGS > "$OUT/pmc_$C.log" 2>&1
+  done
+  (cd "$R" && python tools/pmc_traffic.py "$OUT" --n 65536 --out "$OUT/pmc_traffic_n65536.json" > /dev/null)
+  python "$R/tools/sq_summary.py" "$OUT" --out "$OUT/sq_counters.json" > /dev/null
+fi
+if [ "${PMC4M:-0}" = 1 ]; then  # the true-HBM point: 4 194 304 envs (> 256 MiB MALL)
+  mkdir -p "$OUT/n4m"
+  for C in FETCH_SIZE WRITE_SIZE; do
+    step pmc4m_$C 180 rocprofv3 --pmc $C --output-format csv -d "$OUT/n4m/pmc_$C" -o pmc -- python "$R/bench.py" --no-cpu-baseline --n 4194304 --steps 64 --warmup 8 > "$OUT/n4m/pmc_$C.log" 2>&1
+  done
+  (cd "$R" && python tools/pmc_traffic.py "$OUT/n4m" --n 4194304 --out "$OUT/pmc_traffic_n4194304.json" > /dev/null)
+  for i in 1 2 3; do
+    step bench4m_$i 200 python "$R/bench.py" --no-cpu-baseline --n 4194304 --steps 500 --warmup 20 > "$OUT/bench_n4194304_$i.json" 2> "$OUT/bench_n4194304_$i.err"
   done
 fi
 echo done

@@ -15,6 +15,9 @@ import glob
 import json
 import os
 import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def median_counter(d, name):
@@ -47,6 +50,7 @@ def main():
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), median over step_kernel "
                   "dispatches of bench.py; FETCH_SIZE x2 (gfx950 half-count), KiB = 1024 B",
         "source": a.run_dir,
+        "source_hash": __import__("rl_rocket_amd.build", fromlist=["source_hash"]).source_hash(),
     }
     print(json.dumps(res, indent=1))
     if a.out:
