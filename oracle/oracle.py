@@ -18,7 +18,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librocket_oracle.so")
+LIB_PATH = os.environ.get("RO_LIB_PATH") or os.path.join(HERE, "librocket_oracle.so")  # override: sanitizer builds (tools/sanitize.sh)
 
 # configuration_file.py:4-34 of the reference (the benchmark config), restated as data.
 ENV_CONFIG_6DOF = {

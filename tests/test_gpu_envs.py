@@ -177,7 +177,7 @@ def test_reward_annealing_flag_vs_reference_terms(model, golden6, golden3):
 
     g = golden6 if model == 6 else golden3
     kw = ENV_CONFIG_6DOF if model == 6 else {}
-    xi = make_config(model, **kw).kwargs["reward_coeff"]["xi"]
+    xi = make_config(model, **kw).kwargs["reward_coeff"].get("xi", 0.01)  # RewardAnnealing's default
     out = run_rows(model, g, reward_annealing=True, **kw)
     names = make_config(model, **kw).term_names
     att, goal = names.index("attitude_constraint"), names.index("rew_goal")
