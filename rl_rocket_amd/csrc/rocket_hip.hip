@@ -59,6 +59,15 @@ namespace {
 // state planes, which the next launch re-reads, is slower; nt loads +5 %).
 #define RR_OUT_AUX 16
 #endif
+#ifndef RR_PLANE_REMAT
+#define RR_PLANE_REMAT 0
+#endif
+#ifndef RR_HOT_VGPR  // 1 = the post-integration scalar parameters pinned in VGPRs (0: SGPRs)
+#define RR_HOT_VGPR 0
+#endif
+#ifndef RR_CL_PIN  // 0 = counter layout read where used, 1 = pinned in SGPRs, 2 = in VGPRs
+#define RR_CL_PIN 1
+#endif
 #ifndef RR_STEP_ATTR  // occupancy floor of the step kernel: <= 128 VGPRs keeps 4 waves per SIMD at large N
 #define RR_STEP_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
@@ -112,7 +121,6 @@ constexpr uint32_t kModeCounter = 0x80000000u;
 struct KParams {
     int32_t max_steps;
     uint32_t flags;
-    uint32_t el_mask, ep_shift; // counter word: elapsed = cw & el_mask, episode = cw >> ep_shift
     float h, h2, h6;          // dt, dt/2, dt/6
     float ic_low[RR_MAX_STATE];
     float ic_span[RR_MAX_STATE];
@@ -131,6 +139,10 @@ struct KParams {
     float zero_h;             // x <= 1e-3 as a float threshold
     uint32_t seed_w[4];       // reset stream key words (rr_seed)
     int64_t id_off;           // global id of env 0 (multi-GPU shards)
+    // counter word: elapsed = cw & el_mask, episode = cw >> ep_shift. Last in the struct: placed
+    // after `flags` they shifted the fields above and the kernel's kernarg scalar loads regrouped
+    // (+2 % per step at N = 65536, A/B r02l)
+    uint32_t el_mask, ep_shift;
 };
 
 // The parameters read after the integration (reward, bounds, obs). Copied out of the
@@ -174,9 +186,15 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
         asm volatile("" : "+v"(H.att_c[j]));
         asm volatile("" : "+v"(H.land_c[j]));
     }
+#if RR_HOT_VGPR
+#define RR_HOT(f) \
+    H.f = P.f;    \
+    asm volatile("" : "+v"(H.f))
+#else
 #define RR_HOT(f) \
     H.f = P.f;    \
     pin_s(H.f)
+#endif
     RR_HOT(half_thrust);
     RR_HOT(alfa);
     RR_HOT(beta);
@@ -1051,18 +1069,45 @@ __device__ __forceinline__ bool physics_step(const KParams& P, const float* a, c
     return event;
 }
 
-// gym TimeLimit (main_6DOF.py:21): elapsed += 1; at the limit done = True and
-// info["TimeLimit.truncated"] = not done. Returns the new elapsed count.
-__device__ __forceinline__ int32_t time_limit(const KParams& P, uint32_t cw, bool& done, bool& trunc)
-{
-    const int32_t el = (int32_t)(cw & P.el_mask) + 1;
-    trunc = false;
-    if (P.max_steps > 0 && el >= P.max_steps) {
-        trunc = !done;
-        done = true;
+// The counter-word layout and the TimeLimit, read from the kernel arguments once at kernel
+// start and pinned in SGPRs (pin_s): read where they are used, after the integration, they
+// were scalar loads with a wait in the tail of a lone wave (+2 % per step at N = 65536).
+struct CounterLayout {
+    uint32_t el_mask, ep_shift;
+    int32_t max_steps;
+    __device__ __forceinline__ explicit CounterLayout(const KParams& P)
+        : el_mask(P.el_mask), ep_shift(P.ep_shift), max_steps(P.max_steps)
+    {
+#if RR_CL_PIN == 1
+        pin_s(el_mask);
+        pin_s(ep_shift);
+        pin_s(max_steps);
+#elif RR_CL_PIN == 2
+        asm volatile("" : "+v"(el_mask));
+        asm volatile("" : "+v"(ep_shift));
+        asm volatile("" : "+v"(max_steps));
+#endif
     }
-    return el;
-}
+    // gym TimeLimit (main_6DOF.py:21): elapsed += 1; at the limit done = True and
+    // info["TimeLimit.truncated"] = not done. Returns the new elapsed count.
+    __device__ __forceinline__ int32_t time_limit(uint32_t cw, bool& done, bool& trunc) const
+    {
+        const int32_t el = (int32_t)(cw & el_mask) + 1;
+        trunc = false;
+        if (max_steps > 0 && el >= max_steps) {
+            trunc = !done;
+            done = true;
+        }
+        return el;
+    }
+    // the counter word of a reset env: episode + 1, elapsed 0
+    __device__ __forceinline__ uint32_t next_episode(uint32_t cw) const { return ((cw >> ep_shift) + 1u) << ep_shift; }
+    // the elapsed field set to `el`
+    __device__ __forceinline__ uint32_t with_elapsed(uint32_t cw, int32_t el) const
+    {
+        return (cw & ~el_mask) | ((uint32_t)el & el_mask);
+    }
+};
 
 // terminal obs / return / length of a done env (info["terminal_observation"], Monitor):
 // row i of [N][NS] as 16-B stores (rows are 4-B aligned; gfx950 buffer stores need only
@@ -1128,7 +1173,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
     const Bufs B, const StepIO io)
 {
-    constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT;
+    constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
     constexpr int OW = ROWS ? NS + 2 : NS;  // floats per output row
     __shared__ __attribute__((aligned(16))) float lds[WPB][kWave * OW];
     constexpr int kCandRow = (NS + 1 + 3) / 4 * 4;
@@ -1184,6 +1229,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     float v0 = bld_f(st_r, vo, v0_off);
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
+    const CounterLayout CL(P);
     // SB3 auto-reset candidate of this step, keyed on (gid, counter word): ~190 VALU right
     // after the counter word lands, instead of in the done branch of the waves that finish
     // last. Used by done lanes only. (HELP: drawn by the helper wave instead.)
@@ -1198,7 +1244,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     float t[NT];
     const float r = reward_terms<MODEL>(H, y1, a, v0, bv, t);
     bool done = event || bv, trunc;
-    int32_t el = time_limit(P, cw, done, trunc);
+    int32_t el = CL.time_limit(cw, done, trunc);
     ret += r;
     float o[NS];
     normalize_obs<NS>(y1, H.inv_norm, o);
@@ -1225,19 +1271,25 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
                 v0 = ic_v0;
             }
             bst_f(st_r, v0, vo, v0_off);
-            cw = ((cw >> P.ep_shift) + 1u) << P.ep_shift;
+            cw = CL.next_episode(cw);
             normalize_obs<NS>(y1, H.inv_norm, o);
             el = 0;
             ret = 0.0f;
         }
     }
-    cw = (cw & ~P.el_mask) | ((uint32_t)el & P.el_mask);
+    cw = CL.with_elapsed(cw, el);
 
     if (valid) {
+#if RR_PLANE_REMAT  // plane offsets recomputed here instead of kept live in SGPRs since the loads
+        uint32_t pl = plane;
+        asm volatile("" : "+s"(pl));
+#else
+        const uint32_t pl = plane;
+#endif
 #pragma unroll
-        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
-        if (use_counter) bst_u(st_r, cw, vo, cw_off);
-        if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, ret_off);
+        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * pl);
+        if (use_counter) bst_u(st_r, cw, vo, (NS + 1) * pl);
+        if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, (NS + 2) * pl);
         store_outputs<NT, !ROWS>(io, i, vo, plane, n, r, done, trunc, t, bv, event);
     }
     const uint32_t nvalid = (n - wave_base) < (uint32_t)kWave ? (n - wave_base) : (uint32_t)kWave;
