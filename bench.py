@@ -360,12 +360,14 @@ def main():
             one(k)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    # device time per launch over the timed region (kernel + inter-kernel gap inside the
-    # graph: an upper bound on the kernel's own duration, so `achieved` is conservative)
-    kern_ms = ev0.elapsed_time(ev1) / K
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    # device time per launch over the timed region (kernel + inter-kernel gap inside the
+    # graph: an upper bound on the kernel's own duration, so `achieved` is conservative).
+    # (Events recorded with hipEventReleaseToDevice instead of torch's system-scope release
+    # read the same at K = 20: 4.58 vs 4.56 us per launch, r02o.)
+    kern_ms = ev0.elapsed_time(ev1) / K
     if dist is not None:  # max over ranks of the timed region
         t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
