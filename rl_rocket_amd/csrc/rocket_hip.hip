@@ -225,6 +225,7 @@ struct Bufs {
     float* term_ret;
     int32_t* term_len;
     int64_t n;
+    const KParams* kp;        // device copy of the kernel's KParams (helper waves read it: see step_kernel)
 };
 
 struct StepIO {
@@ -1188,11 +1189,15 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
         if (wv < (uint32_t)WPB && lane == 0) cflag[wv] = 0u;
         __syncthreads();  // flags cleared before any helper can publish
         if (wv >= (uint32_t)WPB) {
+            // the helper role reads its parameters through the device copy (B.kp): kernel-argument
+            // values it used were loaded in the kernel's entry block and kept live into the main
+            // role, where SGPRs are the scarce resource
+            const KParams& P = *B.kp;
             const uint32_t k = wv - WPB;  // the main wave this helper serves
             const uint32_t base = (blockIdx.x * WPB + k) * kWave;
+            const uint32_t ih = min(base + lane, n - 1);
+            const uint32_t cwh = (base < n && (mode & kModeCounter)) ? at(B.counter, ih) : 0u;
             if ((mode & RR_FLAG_AUTO_RESET) && base < n) {
-                const uint32_t ih = min(base + lane, n - 1);
-                const uint32_t cwh = (mode & kModeCounter) ? at(B.counter, ih) : 0u;
                 float s_[NS], v_;
                 ResetStream key = reset_stream(P.seed_w, P.id_off + base + lane, cwh);
                 sample_ic<MODEL>(P, key, s_, v_);
@@ -1538,6 +1543,7 @@ struct rr_env {
     float* term_ret;
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
+    KParams* d_kp;      // device copy of kp (Bufs.kp)
     int32_t* g_idx;     // rr_fetch_done scratch
     float* g_obs;
     float* g_ret;
@@ -1558,6 +1564,7 @@ Bufs bufs_of(const rr_env* e)
     b.term_ret = e->term_ret;
     b.term_len = e->term_len;
     b.n = e->n;
+    b.kp = e->d_kp;
     return b;
 }
 
@@ -1653,6 +1660,13 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->counter = reinterpret_cast<uint32_t*>(e->state + (size_t)(e->ns + 1) * n);
     e->ep_ret = e->state + (size_t)(e->ns + 2) * n;
     e->kp.id_off = env_id_offset;
+    {
+        hipError_t err = hipMalloc((void**)&e->d_kp, sizeof(KParams));
+        if (err != hipSuccess) {
+            rr_destroy(e);
+            return hip_fail(err, "rr_create: hipMalloc (params)");
+        }
+    }
     int rc = rr_seed(e, 42, nullptr);
     if (rc == RR_OK) {
         hipError_t err = hipDeviceSynchronize();
@@ -1670,7 +1684,7 @@ int rr_destroy(rr_env* e)
 {
     if (!e) return RR_OK;
     DeviceGuard g(e->device);
-    void* ptrs[] = {e->state, e->state64, e->done_bits,
+    void* ptrs[] = {e->state, e->state64, e->d_kp, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -1684,10 +1698,13 @@ int rr_action_dim(const rr_env* e) { return e ? e->na : -1; }
 
 int rr_seed(rr_env* e, uint64_t seed, void* stream)
 {
-    (void)stream;  // the reset stream is counter-based: the seed is a kernel argument
+    // the reset stream is counter-based: the seed is a kernel argument, and helper waves read it
+    // from the device copy, updated in stream order (it applies to every later launch)
     if (!e) return fail(RR_EINVAL, "rr_seed: null handle");
     seed_words(seed, e->kp.seed_w);
-    return RR_OK;
+    hipError_t err = hipMemcpyAsync(e->d_kp, &e->kp, sizeof(KParams), hipMemcpyHostToDevice, (hipStream_t)stream);
+    if (err == hipSuccess) err = hipStreamSynchronize((hipStream_t)stream);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_seed: params upload");
 }
 
 int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
