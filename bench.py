@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--model", default="6DOF")
     ap.add_argument("--integrator", default="rk4")
     ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--monitor", action="store_true",
+                    help="the drop-in default (RocketVecEnv monitor=True): Monitor running return kept per env "
+                         "(read + written every step, +8 B per env-step); the headline runs without it")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--launch", default="graph", choices=["graph", "loop"],
                     help="graph: K launches replayed from hipGraphs; loop: one rr_step_repeat call (K launches "
@@ -288,7 +291,7 @@ def main():
             dist.destroy_process_group()
         return
     env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
-                      episode_stats=False, integrator=args.integrator, env_id_offset=rank * n, **kw)
+                      episode_stats=args.monitor, integrator=args.integrator, env_id_offset=rank * n, **kw)
     env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
@@ -374,9 +377,13 @@ def main():
         dt = float(t.item())
 
     value = n * world * K / dt
-    bytes_launch = BYTES_PER_STEP[model] * n
+    bytes_env = BYTES_PER_STEP[model] + (8 if args.monitor else 0)  # + Monitor return plane read / write
+    bytes_launch = bytes_env * n
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = stored_traffic(model, n)
+    if args.monitor or args.allgather or args.integrator != "rk4":
+        traffic, traffic_src = None, "PMC traffic files cover the headline configuration (RK4, no Monitor, no gather)"
+    else:
+        traffic, traffic_src = stored_traffic(model, n)
     result = {
         "metric": "env-steps/sec (%s, N=%d per GPU)" % ("6DOF" if model == 6 else "3DOF", n),
         "value": value,
@@ -394,7 +401,7 @@ def main():
         "config": {"workload": "Rocket%s N=%d per GPU, %s fused step+reward+TimeLimit(800)+auto-reset, %s"
                                % ("6DOF" if model == 6 else "3DOF", n, args.integrator.upper(),
                                   "step rows + RCCL all_gather of obs/reward/done each step" if args.allgather else
-                                  "no data-path collective"),
+                                  "no data-path collective") + (", Monitor returns" if args.monitor else ""),
                    "envs_per_gpu": n, "global_envs": n * world, "integrator": args.integrator,
                    "graph_steps": gs if use_graph else 0, "launch": "graph" if use_graph else
                    ("rr_step_repeat" if use_loop else "rr_step per step"),
@@ -408,7 +415,7 @@ def main():
                                (" (each step = rr_step_rows + the RCCL all_gather, so kernel_us includes the "
                                 "collective)" if gather is not None else ""),
                      "bytes_per_launch": bytes_launch,
-                     "bytes_per_env_step": BYTES_PER_STEP[model]},
+                     "bytes_per_env_step": bytes_env},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baselines(model, args.cpu_seconds, host_cores())

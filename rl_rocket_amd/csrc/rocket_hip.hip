@@ -44,6 +44,12 @@ namespace {
 #ifndef RR_OBS_PACKED
 #define RR_OBS_PACKED 1
 #endif
+#ifndef RR_TOUCH_TAIL_ARGS  // 1 = read the tail's pointer arguments early (scalar cache warm)
+#define RR_TOUCH_TAIL_ARGS 1
+#endif
+#ifndef RR_HOT_EARLY  // 1 = hot-parameter copies scheduled before the first use of the loaded state
+#define RR_HOT_EARLY 1
+#endif
 #ifndef RR_NEWTON_ITERS
 #define RR_NEWTON_ITERS 3
 #endif
@@ -1235,6 +1241,20 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
     const CounterLayout CL(P);
+#if RR_TOUCH_TAIL_ARGS
+    // the kernel-argument lines holding the tail's pointers (outputs, terminal rows) are read
+    // here, in the load shadow, so that the scalar reloads after the integration hit the
+    // scalar cache instead of missing in the wave's critical tail (HELP kernels: without the
+    // helpers' device parameter copy the SGPRs are short, 2-5 spills)
+    if constexpr (HELP)
+        asm volatile("" ::"s"(io.obs), "s"(io.reward), "s"(io.done), "s"(io.truncated), "s"(B.done_bits),
+                     "s"(B.term_obs));
+#endif
+#if RR_HOT_EARLY
+    // the SGPR -> VGPR copies of the pinned per-axis parameters issue here, in the shadow of
+    // the state loads; left to the scheduler they landed after the load wait, inside the RK4
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     // SB3 auto-reset candidate of this step, keyed on (gid, counter word): ~190 VALU right
     // after the counter word lands, instead of in the done branch of the waves that finish
     // last. Used by done lanes only. (HELP: drawn by the helper wave instead.)

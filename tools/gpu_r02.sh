@@ -30,10 +30,16 @@ for i in 1 2 3; do
 done
 step bench_k2000 300 python bench.py --no-cpu-baseline $BENCH_ARGS > "$OUT/bench_k2000.json" 2> "$OUT/bench_k2000.err"
 cat "$OUT/bench_k2000.json"
+# the drop-in default configuration (RocketVecEnv monitor=True: Monitor return plane per step)
+step bench_monitor_k20 300 python bench.py --no-cpu-baseline --monitor --steps 20 --warmup 5 > "$OUT/bench_monitor_k20.json" 2> "$OUT/bench_monitor_k20.err"
+step bench_monitor_k2000 300 python bench.py --no-cpu-baseline --monitor > "$OUT/bench_monitor_k2000.json" 2> "$OUT/bench_monitor_k2000.err"
 export TMPDIR=/tmp
 cd /tmp || exit 2
 step rocprof_k20 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_k20" -o bench -- python "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_k20.log" 2>&1
 step rocprof_k2000 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_k2000" -o bench -- python "$R/bench.py" --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_k2000.log" 2>&1
+# isolated dispatches (direct launches, host-paced): kernel-trace durations without the
+# profiler's back-to-back completion handling inside them
+step rocprof_loop 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_loop" -o bench -- python "$R/bench.py" --no-cpu-baseline --launch loop --steps 2000 --warmup 20 $BENCH_ARGS > "$OUT/prof_loop.log" 2>&1
 if [ "${PMC:-1}" = 1 ]; then
   step pmc_SQ 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmc_SQ" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $BENCH_ARGS > "$OUT/pmc_SQ.log" 2>&1
   step pmc_SQ2 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32 --output-format csv -d "$OUT/pmc_SQ2" -o pmc -- python "$R/bench.py" --no-cpu-baseline --steps 256 --warmup 20 $BENCH_ARGS > "$OUT/pmc_SQ2.log" 2>&1
@@ -46,6 +52,8 @@ if [ "${PMC:-1}" = 1 ]; then
 fi
 if [ "${PMC4M:-0}" = 1 ]; then  # the true-HBM point: 4 194 304 envs (> 256 MiB MALL)
   mkdir -p "$OUT/n4m"
+  step hbm_probe 120 python "$R/tools/hbm_probe.py" > "$OUT/hbm_probe.json" 2> "$OUT/hbm_probe.err"
+  cat "$OUT/hbm_probe.json"
   for C in FETCH_SIZE WRITE_SIZE; do
     step pmc4m_$C 180 rocprofv3 --pmc $C --output-format csv -d "$OUT/n4m/pmc_$C" -o pmc -- python "$R/bench.py" --no-cpu-baseline --n 4194304 --steps 64 --warmup 8 > "$OUT/n4m/pmc_$C.log" 2>&1
   done

@@ -1,0 +1,138 @@
+"""Where one step's time goes, per wave: a diagnostic copy of the step kernel with
+s_memrealtime stamps (100 MHz) at four points of every main wave, built OUTSIDE the product
+source (the product kernel carries no diagnostic code).
+
+    python tools/stamp_probe.py build          # here: writes .ab/stamp.so from a patched copy
+    python tools/stamp_probe.py run [--k 20]   # GPU box: K graph launches, stamps of the last
+
+Stamps per main wave: t0 wave start, t1 state / action / counter loads landed, t2 reward +
+obs computed, t3 every store of the wave acknowledged (s_waitcnt vmcnt(0) after the last
+store). Printed relative to the earliest t0 of the launch, with the HIP-event time of the
+same launches for the launch floor around them.
+"""
+import argparse
+import ctypes
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, ".ab", "stamp.so")
+
+
+def patch(src):
+    def sub(pattern, repl, count=1):
+        nonlocal src
+        new, k = re.subn(pattern, repl.replace('\\"', '"'), src, count=count)
+        if k != count:
+            raise SystemExit("stamp_probe: pattern not found: %r" % pattern)
+        src = new
+
+    sub(r"(namespace \{\n)", r"\1__device__ unsigned long long g_stamps[4 * 65536];\n")
+    sub(r"(    const bool valid = i < n;\n)",
+        r"\1    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();\n")
+    sub(r"(    const CounterLayout CL\(P\);\n)",
+        r"\1    asm volatile(\"; loads used\" ::\"v\"(y0[0]), \"v\"(y0[6]), \"v\"(y0[13]), \"v\"(a[0]), \"v\"(a[2]), "
+        r"\"v\"(v0), \"v\"(cw));\n    const unsigned long long st1 = __builtin_amdgcn_s_memrealtime();\n")
+    sub(r"(    float o\[NS\];\n    normalize_obs<NS>\(y1, H.inv_norm, o\);\n)",
+        r"\1    asm volatile(\"; computed\" ::\"v\"(o[0]), \"v\"(o[13]), \"v\"(r));\n"
+        r"    const unsigned long long st2 = __builtin_amdgcn_s_memrealtime();\n")
+    sub(r"(        store_obs_tile<NS, kWave>\(lds\[wv\], o, make_rsrc\(io.obs, \(uint64_t\)NS \* plane\), wave_base, lane, "
+        r"nvalid,\n                                  io.obs_vec_ok\);\n    \}\n)",
+        r"\1    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
+        r"    const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();\n"
+        r"    if (lane == 0 && wave_idx < 65536u) {\n"
+        r"        g_stamps[4 * wave_idx] = st0;\n        g_stamps[4 * wave_idx + 1] = st1;\n"
+        r"        g_stamps[4 * wave_idx + 2] = st2;\n        g_stamps[4 * wave_idx + 3] = st3;\n    }\n")
+    sub(r"(extern \"C\" \{\n)", r"\1void* rr_diag_stamps() { void* p = nullptr; "
+        r"(void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)); return p; }\n")
+    return src
+
+
+def build():
+    from rl_rocket_amd import build as b
+
+    src = patch(open(b.SRC).read())
+    tmp = os.path.join(ROOT, ".ab", "stamp_src")
+    os.makedirs(tmp, exist_ok=True)
+    for f in [os.path.basename(p) for p in b.DEPS]:
+        with open(os.path.join(b.HERE, "csrc", f)) as fi, open(os.path.join(tmp, f), "w") as fo:
+            fo.write(fi.read())
+    path = os.path.join(tmp, "rocket_hip.hip")
+    with open(path, "w") as f:
+        f.write(src)
+    cmd = b.command(out=OUT)
+    cmd[-1] = path
+    subprocess.check_call(cmd, cwd=ROOT)
+    print(OUT)
+
+
+def run(k, n):
+    os.environ["RR_LIB_PATH"] = OUT
+    import numpy as np
+    import torch
+
+    from rl_rocket_amd import _lib
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+
+    lib = _lib.load()
+    lib.rr_diag_stamps.restype = ctypes.c_void_p
+    dev = torch.device("cuda", 0)
+    env = RocketBatch(n, model=6, device=dev, max_episode_steps=800, auto_reset=True, episode_stats=False,
+                      **ENV_CONFIG_6DOF)
+    env.reset()
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    pool = torch.rand((8, n, 3), device=dev, generator=g) * 2 - 1
+    for j in range(30):
+        env.step(pool[j % 8])
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(gr, stream=s):
+            for j in range(k):
+                env.step(pool[j % 8])
+    torch.cuda.current_stream(dev).wait_stream(s)
+    gr.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    gr.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    waves = n // 64
+    hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    buf = np.zeros(4 * waves, dtype=np.uint64)
+    rc = hip.hipMemcpy(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(lib.rr_diag_stamps()),
+                       ctypes.c_size_t(buf.nbytes), ctypes.c_int(2))
+    if rc != 0:
+        raise SystemExit("hipMemcpy failed: %d" % rc)
+    st = buf.reshape(waves, 4).astype(np.int64)
+    t = (st - st[:, 0].min()) * 10  # ns
+    q = lambda a: {p: float(np.percentile(a, p)) for p in (0, 50, 90, 99, 100)}  # noqa: E731
+    print(json.dumps({
+        "k": k, "n": n, "event_us_per_launch": e0.elapsed_time(e1) * 1e3 / k,
+        "ns_start": q(t[:, 0]), "ns_loads_landed": q(t[:, 1] - t[:, 0]), "ns_compute": q(t[:, 2] - t[:, 1]),
+        "ns_tail_to_ack": q(t[:, 3] - t[:, 2]), "ns_wave_total": q(t[:, 3] - t[:, 0]),
+        "ns_last_ack_after_first_start": float(t[:, 3].max()),
+        "slowest_wave": {"index": int(np.argmax(t[:, 3])), "stamps_ns": t[int(np.argmax(t[:, 3]))].tolist()},
+    }, indent=1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["build", "run"])
+    ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--n", type=int, default=65536)
+    a = ap.parse_args()
+    build() if a.what == "build" else run(a.k, a.n)
+
+
+if __name__ == "__main__":
+    main()
