@@ -6,8 +6,9 @@ source (the product kernel carries no diagnostic code).
     python tools/stamp_probe.py run [--k 20]   # GPU box: K graph launches, stamps of the last
 
 Stamps per main wave: t0 wave start, t1 state / action / counter loads landed, t2 reward +
-obs computed, t3 every store of the wave acknowledged (s_waitcnt vmcnt(0) after the last
-store). Printed relative to the earliest t0 of the launch, with the HIP-event time of the
+obs computed, t4 done mask / terminal rows / auto-reset done, t5 state planes and outputs
+issued, t6 obs tile issued, t3 every store of the wave acknowledged (s_waitcnt vmcnt(0) after
+the last store). Printed relative to the earliest t0 of the launch, with the HIP-event time of the
 same launches for the launch floor around them.
 """
 import argparse
@@ -31,7 +32,7 @@ def patch(src):
             raise SystemExit("stamp_probe: pattern not found: %r" % pattern)
         src = new
 
-    sub(r"(namespace \{\n)", r"\1__device__ unsigned long long g_stamps[4 * 65536];\n")
+    sub(r"(namespace \{\n)", r"\1__device__ unsigned long long g_stamps[8 * 65536];\n")
     sub(r"(    const bool valid = i < n;\n)",
         r"\1    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();\n")
     sub(r"(    const CounterLayout CL\(P\);\n)",
@@ -40,13 +41,18 @@ def patch(src):
     sub(r"(    float o\[NS\];\n    normalize_obs<NS>\(y1, H.inv_norm, o\);\n)",
         r"\1    asm volatile(\"; computed\" ::\"v\"(o[0]), \"v\"(o[13]), \"v\"(r));\n"
         r"    const unsigned long long st2 = __builtin_amdgcn_s_memrealtime();\n")
+    sub(r"(    cw = CL.with_elapsed\(cw, el\);\n)",
+        r"\1    const unsigned long long st4 = __builtin_amdgcn_s_memrealtime();\n")
+    sub(r"(        store_outputs<NT, !ROWS>\(io, i, vo, plane, n, r, done, trunc, t, bv, event\);\n    \}\n)",
+        r"\1    const unsigned long long st5 = __builtin_amdgcn_s_memrealtime();\n")
     sub(r"(        store_obs_tile<NS, kWave>\(lds\[wv\], o, make_rsrc\(io.obs, \(uint64_t\)NS \* plane\), wave_base, lane, "
         r"nvalid,\n                                  io.obs_vec_ok\);\n    \}\n)",
-        r"\1    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
+        r"\1    const unsigned long long st6 = __builtin_amdgcn_s_memrealtime();\n"
+        r"    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
         r"    const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();\n"
         r"    if (lane == 0 && wave_idx < 65536u) {\n"
-        r"        g_stamps[4 * wave_idx] = st0;\n        g_stamps[4 * wave_idx + 1] = st1;\n"
-        r"        g_stamps[4 * wave_idx + 2] = st2;\n        g_stamps[4 * wave_idx + 3] = st3;\n    }\n")
+        r"        unsigned long long* g = g_stamps + 8 * wave_idx;\n"
+        r"        g[0] = st0; g[1] = st1; g[2] = st2; g[3] = st3; g[4] = st4; g[5] = st5; g[6] = st6;\n    }\n")
     sub(r"(extern \"C\" \{\n)", r"\1void* rr_diag_stamps() { void* p = nullptr; "
         r"(void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)); return p; }\n")
     return src
@@ -108,18 +114,20 @@ def run(k, n):
     torch.cuda.synchronize()
     waves = n // 64
     hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
-    buf = np.zeros(4 * waves, dtype=np.uint64)
+    buf = np.zeros(8 * waves, dtype=np.uint64)
     rc = hip.hipMemcpy(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(lib.rr_diag_stamps()),
                        ctypes.c_size_t(buf.nbytes), ctypes.c_int(2))
     if rc != 0:
         raise SystemExit("hipMemcpy failed: %d" % rc)
-    st = buf.reshape(waves, 4).astype(np.int64)
+    st = buf.reshape(waves, 8)[:, :7].astype(np.int64)
     t = (st - st[:, 0].min()) * 10  # ns
     q = lambda a: {p: float(np.percentile(a, p)) for p in (0, 50, 90, 99, 100)}  # noqa: E731
     print(json.dumps({
         "k": k, "n": n, "event_us_per_launch": e0.elapsed_time(e1) * 1e3 / k,
         "ns_start": q(t[:, 0]), "ns_loads_landed": q(t[:, 1] - t[:, 0]), "ns_compute": q(t[:, 2] - t[:, 1]),
         "ns_tail_to_ack": q(t[:, 3] - t[:, 2]), "ns_wave_total": q(t[:, 3] - t[:, 0]),
+        "ns_done_reset": q(t[:, 4] - t[:, 2]), "ns_state_output_issue": q(t[:, 5] - t[:, 4]),
+        "ns_obs_tile_issue": q(t[:, 6] - t[:, 5]), "ns_ack_wait": q(t[:, 3] - t[:, 6]),
         "ns_last_ack_after_first_start": float(t[:, 3].max()),
         "slowest_wave": {"index": int(np.argmax(t[:, 3])), "stamps_ns": t[int(np.argmax(t[:, 3]))].tolist()},
     }, indent=1))
