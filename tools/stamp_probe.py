@@ -41,6 +41,9 @@ def patch(src):
     sub(r"(    float o\[NS\];\n    normalize_obs<NS>\(y1, H.inv_norm, o\);\n)",
         r"\1    asm volatile(\"; computed\" ::\"v\"(o[0]), \"v\"(o[13]), \"v\"(r));\n"
         r"    const unsigned long long st2 = __builtin_amdgcn_s_memrealtime();\n")
+    sub(r"(        if \(dv\) store_terminal<NS>\(B, i, vo, plane, o, ret, el\);\n)",
+        r"\1        st7 = __builtin_amdgcn_s_memrealtime();\n")
+    sub(r"(    const uint64_t m = __ballot\(dv\);\n)", r"\1    unsigned long long st7 = 0;\n")
     sub(r"(    cw = CL.with_elapsed\(cw, el\);\n)",
         r"\1    const unsigned long long st4 = __builtin_amdgcn_s_memrealtime();\n")
     sub(r"(        store_outputs<NT, !ROWS>\(io, i, vo, plane, n, r, done, trunc, t, bv, event\);\n    \}\n)",
@@ -52,7 +55,8 @@ def patch(src):
         r"    const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();\n"
         r"    if (lane == 0 && wave_idx < 65536u) {\n"
         r"        unsigned long long* g = g_stamps + 8 * wave_idx;\n"
-        r"        g[0] = st0; g[1] = st1; g[2] = st2; g[3] = st3; g[4] = st4; g[5] = st5; g[6] = st6;\n    }\n")
+        r"        g[0] = st0; g[1] = st1; g[2] = st2; g[3] = st3; g[4] = st4; g[5] = st5; g[6] = st6; g[7] = st7;\n"
+        r"    }\n")
     sub(r"(extern \"C\" \{\n)", r"\1void* rr_diag_stamps() { void* p = nullptr; "
         r"(void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)); return p; }\n")
     return src
@@ -119,8 +123,9 @@ def run(k, n):
                        ctypes.c_size_t(buf.nbytes), ctypes.c_int(2))
     if rc != 0:
         raise SystemExit("hipMemcpy failed: %d" % rc)
-    st = buf.reshape(waves, 8)[:, :7].astype(np.int64)
-    t = (st - st[:, 0].min()) * 10  # ns
+    st = buf.reshape(waves, 8).astype(np.int64)
+    t = (st[:, :7] - st[:, 0].min()) * 10  # ns
+    has_done = st[:, 7] > 0
     q = lambda a: {p: float(np.percentile(a, p)) for p in (0, 50, 90, 99, 100)}  # noqa: E731
     print(json.dumps({
         "k": k, "n": n, "event_us_per_launch": e0.elapsed_time(e1) * 1e3 / k,
@@ -128,6 +133,9 @@ def run(k, n):
         "ns_tail_to_ack": q(t[:, 3] - t[:, 2]), "ns_wave_total": q(t[:, 3] - t[:, 0]),
         "ns_done_reset": q(t[:, 4] - t[:, 2]), "ns_state_output_issue": q(t[:, 5] - t[:, 4]),
         "ns_obs_tile_issue": q(t[:, 6] - t[:, 5]), "ns_ack_wait": q(t[:, 3] - t[:, 6]),
+        "waves_with_done": int(has_done.sum()),
+        "ns_terminal_rows_done_waves": q((st[has_done, 7] - st[has_done, 2]) * 10) if has_done.any() else None,
+        "ns_reset_after_terminal_done_waves": q((st[has_done, 4] - st[has_done, 7]) * 10) if has_done.any() else None,
         "ns_last_ack_after_first_start": float(t[:, 3].max()),
         "slowest_wave": {"index": int(np.argmax(t[:, 3])), "stamps_ns": t[int(np.argmax(t[:, 3]))].tolist()},
     }, indent=1))
