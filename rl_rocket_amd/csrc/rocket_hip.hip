@@ -32,27 +32,15 @@
 
 namespace {
 
-// Cache-policy bits of the step kernel's buffer loads / stores (gfx950 CPol: 1 = sc0,
-// 2 = nt, 16 = sc1); 0 = default policy. RR_ST_AUX: library state planes; RR_OUT_AUX:
-// caller-owned outputs.
 #ifndef RR_RK4_GENERIC  // 1 = generic 14-component RK4 for 6DOF too (A/B reference)
 #define RR_RK4_GENERIC 0
 #endif
-#ifndef RR_RK4_PACKED  // 1 = 6DOF RK4 on packed fp32 pairs (v_pk_fma_f32)
-#define RR_RK4_PACKED 1
-#endif
-#ifndef RR_OBS_PACKED
-#define RR_OBS_PACKED 1
-#endif
-#ifndef RR_TOUCH_TAIL_ARGS  // 1 = read the tail's pointer arguments early (scalar cache warm)
-#define RR_TOUCH_TAIL_ARGS 1
-#endif
-#ifndef RR_HOT_EARLY  // 1 = hot-parameter copies scheduled before the first use of the loaded state
-#define RR_HOT_EARLY 1
-#endif
-#ifndef RR_NEWTON_ITERS
+#ifndef RR_NEWTON_ITERS  // Newton iterations of the event root (2: -1.2 %, parity margin 36x -> 3x)
 #define RR_NEWTON_ITERS 3
 #endif
+// Cache-policy bits of the step kernel's buffer loads / stores (gfx950 CPol: 1 = sc0,
+// 2 = nt, 16 = sc1); 0 = default policy. RR_ST_AUX: library state planes; RR_OUT_AUX:
+// caller-owned outputs.
 #ifndef RR_LD_AUX
 #define RR_LD_AUX 0
 #endif
@@ -64,15 +52,6 @@ namespace {
 // in the end-of-kernel writeback (A/B at N = 65536: 5.49 -> 5.18 us; the same bit on the
 // state planes, which the next launch re-reads, is slower; nt loads +5 %).
 #define RR_OUT_AUX 16
-#endif
-#ifndef RR_PLANE_REMAT
-#define RR_PLANE_REMAT 0
-#endif
-#ifndef RR_HOT_VGPR  // 1 = the post-integration scalar parameters pinned in VGPRs (0: SGPRs)
-#define RR_HOT_VGPR 0
-#endif
-#ifndef RR_CL_PIN  // 0 = counter layout read where used, 1 = pinned in SGPRs, 2 = in VGPRs
-#define RR_CL_PIN 1
 #endif
 #ifndef RR_STEP_ATTR  // occupancy floor of the step kernel: <= 128 VGPRs keeps 4 waves per SIMD at large N
 #define RR_STEP_ATTR __attribute__((amdgpu_waves_per_eu(4)))
@@ -192,15 +171,9 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
         asm volatile("" : "+v"(H.att_c[j]));
         asm volatile("" : "+v"(H.land_c[j]));
     }
-#if RR_HOT_VGPR
-#define RR_HOT(f) \
-    H.f = P.f;    \
-    asm volatile("" : "+v"(H.f))
-#else
 #define RR_HOT(f) \
     H.f = P.f;    \
     pin_s(H.f)
-#endif
     RR_HOT(half_thrust);
     RR_HOT(alfa);
     RR_HOT(beta);
@@ -471,89 +444,8 @@ __device__ __forceinline__ void rhs(const KParams& P, const Ctl& c, const float*
 // (the RK4 update itself, rearranged); m is linear in t (exact at every stage); w1 is
 // constant (J2 == J3); q and (w2, w3) take the usual RK4 stages, carried as half-rates
 // W = w/2 so dq = Omega(W) q needs no 0.5 factors. Same RK4 solution as the generic form
-// below up to fp32 rounding. f0 = f(y0) for the event path.
-__device__ __forceinline__ void integrate6_rk4(const KParams& P, const Ctl& c, const float* y0, float* y1,
-                                               float* f0)
-{
-    const float h = P.h, hh = P.h2, h6 = P.h6, hh6 = P.h * P.h6;
-    const float t2x = 2.0f * c.tbx, t2y = 2.0f * c.tby, t2z = 2.0f * c.tbz;
-    // R(q) T_b / m + g with the unnormalised q (see rhs)
-    auto accel = [&](const float* q, float m, float* a) {
-        const float qq = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
-        const float tx = q[2] * t2z - q[3] * t2y;
-        const float ty = q[3] * t2x - q[1] * t2z;
-        const float tz = q[1] * t2y - q[2] * t2x;
-        const float sc = frcp(qq * m);
-        a[0] = (qq * c.tbx + q[0] * tx + (q[2] * tz - q[3] * ty)) * sc - kG0;
-        a[1] = (qq * c.tby + q[0] * ty + (q[3] * tx - q[1] * tz)) * sc;
-        a[2] = (qq * c.tbz + q[0] * tz + (q[1] * ty - q[2] * tx)) * sc;
-    };
-    const float W1 = 0.5f * y0[10];
-    // dW2 = A2 + B2 W3, dW3 = A3 + B3 W2 (half of dw = J^-1 (tau - w x Jw))
-    const float A2 = 0.5f * c.tau1, B2 = (-2.0f * kJd1 * kJinv2) * W1;
-    const float A3 = 0.5f * c.tau2, B3 = (-2.0f * kJd2 * kJinv3) * W1;
-    auto dq = [&](const float* q, float W2, float W3, float* d) {
-        d[0] = -W1 * q[1] - W2 * q[2] - W3 * q[3];
-        d[1] = W1 * q[0] + W3 * q[2] - W2 * q[3];
-        d[2] = W2 * q[0] - W3 * q[1] + W1 * q[3];
-        d[3] = W3 * q[0] + W2 * q[1] - W1 * q[2];
-    };
-    const float* q0 = y0 + 6;
-    const float W20 = 0.5f * y0[11], W30 = 0.5f * y0[12], m0 = y0[13];
-    const float mh = m0 + hh * c.dm, me = m0 + h * c.dm;
-    float a1[3], a2[3], a3[3], a4[3], k1[4], k2[4], k3[4], k4[4], qs[4];
-    // stage 1
-    accel(q0, m0, a1);
-    dq(q0, W20, W30, k1);
-    const float l1 = A2 + B2 * W30, n1 = A3 + B3 * W20;
-    // stage 2
-#pragma unroll
-    for (int j = 0; j < 4; ++j) qs[j] = q0[j] + hh * k1[j];
-    float W2s = W20 + hh * l1, W3s = W30 + hh * n1;
-    accel(qs, mh, a2);
-    dq(qs, W2s, W3s, k2);
-    const float l2 = A2 + B2 * W3s, n2 = A3 + B3 * W2s;
-    // stage 3
-#pragma unroll
-    for (int j = 0; j < 4; ++j) qs[j] = q0[j] + hh * k2[j];
-    W2s = W20 + hh * l2;
-    W3s = W30 + hh * n2;
-    accel(qs, mh, a3);
-    dq(qs, W2s, W3s, k3);
-    const float l3 = A2 + B2 * W3s, n3 = A3 + B3 * W2s;
-    // stage 4
-#pragma unroll
-    for (int j = 0; j < 4; ++j) qs[j] = q0[j] + h * k3[j];
-    W2s = W20 + h * l3;
-    W3s = W30 + h * n3;
-    accel(qs, me, a4);
-    dq(qs, W2s, W3s, k4);
-    const float l4 = A2 + B2 * W3s, n4 = A3 + B3 * W2s;
-    // updates
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const float s23 = a2[j] + a3[j];
-        y1[3 + j] = y0[3 + j] + h6 * (a1[j] + a4[j] + 2.0f * s23);
-        y1[j] = (y0[j] + h * y0[3 + j]) + hh6 * (a1[j] + s23);
-        f0[j] = y0[3 + j];
-        f0[3 + j] = a1[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        y1[6 + j] = q0[j] + h6 * (k1[j] + k4[j] + 2.0f * (k2[j] + k3[j]));
-        f0[6 + j] = k1[j];
-    }
-    y1[10] = y0[10];
-    y1[11] = 2.0f * (W20 + h6 * (l1 + l4 + 2.0f * (l2 + l3)));
-    y1[12] = 2.0f * (W30 + h6 * (n1 + n4 + 2.0f * (n2 + n3)));
-    y1[13] = me;
-    f0[10] = 0.0f;
-    f0[11] = 2.0f * l1;
-    f0[12] = 2.0f * n1;
-    f0[13] = c.dm;
-}
-
-// The same specialised RK4 on packed fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32, two lanes'
+// (integrate) up to fp32 rounding. f0 = f(y0) for the event path.
+// It runs on packed fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32, two lanes'
 // worth of fp32 per instruction): a lone wave issues one VALU instruction per 4 cycles
 // whatever its width, so pairing the independent components of one env halves the issue
 // cost of the quaternion and angular-rate algebra. Pairs: q = (q0,q1),(q2,q3);
@@ -563,7 +455,6 @@ __device__ __forceinline__ void integrate6_rk4(const KParams& P, const Ctl& c, c
 template <int NS>
 __device__ __forceinline__ void normalize_obs(const float* y, const float* inv_norm, float* o)
 {
-#if RR_OBS_PACKED
 #pragma unroll
     for (int j = 0; j + 1 < NS; j += 2) {
         const f2 v = f2{y[j], y[j + 1]} * f2{inv_norm[j], inv_norm[j + 1]};
@@ -571,10 +462,6 @@ __device__ __forceinline__ void normalize_obs(const float* y, const float* inv_n
         o[j + 1] = v.y;
     }
     if constexpr (NS % 2) o[NS - 1] = y[NS - 1] * inv_norm[NS - 1];
-#else
-#pragma unroll
-    for (int j = 0; j < NS; ++j) o[j] = y[j] * inv_norm[j];
-#endif
 }
 
 // Packed 6DOF RHS pieces for one step's controls: R(q) T_b / m + g as (ax, ay), az, and
@@ -743,11 +630,7 @@ __device__ __forceinline__ void integrate(const KParams& P, const Ctl& c, const 
     float k[NS], yt[NS];
 #if !RR_RK4_GENERIC
     if constexpr (MODEL == 6 && INTEG == RR_INT_RK4) {
-#if RR_RK4_PACKED
         integrate6_rk4_pk(P, c, y0, y1, f0);
-#else
-        integrate6_rk4(P, c, y0, y1, f0);
-#endif
         return;
     }
 #endif
@@ -1085,15 +968,9 @@ struct CounterLayout {
     __device__ __forceinline__ explicit CounterLayout(const KParams& P)
         : el_mask(P.el_mask), ep_shift(P.ep_shift), max_steps(P.max_steps)
     {
-#if RR_CL_PIN == 1
         pin_s(el_mask);
         pin_s(ep_shift);
         pin_s(max_steps);
-#elif RR_CL_PIN == 2
-        asm volatile("" : "+v"(el_mask));
-        asm volatile("" : "+v"(ep_shift));
-        asm volatile("" : "+v"(max_steps));
-#endif
     }
     // gym TimeLimit (main_6DOF.py:21): elapsed += 1; at the limit done = True and
     // info["TimeLimit.truncated"] = not done. Returns the new elapsed count.
@@ -1241,7 +1118,6 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
     const CounterLayout CL(P);
-#if RR_TOUCH_TAIL_ARGS
     // the kernel-argument lines holding the tail's pointers (outputs, terminal rows) are read
     // here, in the load shadow, so that the scalar reloads after the integration hit the
     // scalar cache instead of missing in the wave's critical tail (HELP kernels: without the
@@ -1249,12 +1125,9 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     if constexpr (HELP)
         asm volatile("" ::"s"(io.obs), "s"(io.reward), "s"(io.done), "s"(io.truncated), "s"(B.done_bits),
                      "s"(B.term_obs));
-#endif
-#if RR_HOT_EARLY
     // the SGPR -> VGPR copies of the pinned per-axis parameters issue here, in the shadow of
     // the state loads; left to the scheduler they landed after the load wait, inside the RK4
     __builtin_amdgcn_sched_barrier(0);
-#endif
     // SB3 auto-reset candidate of this step, keyed on (gid, counter word): ~190 VALU right
     // after the counter word lands, instead of in the done branch of the waves that finish
     // last. Used by done lanes only. (HELP: drawn by the helper wave instead.)
@@ -1305,16 +1178,10 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     cw = CL.with_elapsed(cw, el);
 
     if (valid) {
-#if RR_PLANE_REMAT  // plane offsets recomputed here instead of kept live in SGPRs since the loads
-        uint32_t pl = plane;
-        asm volatile("" : "+s"(pl));
-#else
-        const uint32_t pl = plane;
-#endif
 #pragma unroll
-        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * pl);
-        if (use_counter) bst_u(st_r, cw, vo, (NS + 1) * pl);
-        if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, (NS + 2) * pl);
+        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
+        if (use_counter) bst_u(st_r, cw, vo, (NS + 1) * plane);
+        if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, (NS + 2) * plane);
         store_outputs<NT, !ROWS>(io, i, vo, plane, n, r, done, trunc, t, bv, event);
     }
     const uint32_t nvalid = (n - wave_base) < (uint32_t)kWave ? (n - wave_base) : (uint32_t)kWave;
