@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, ".ab", "stamp.so")
 
 
-def patch(src):
+def patch(src, twice=False):
     def sub(pattern, repl, count=1):
         nonlocal src
         new, k = re.subn(pattern, repl.replace('\\"', '"'), src, count=count)
@@ -33,6 +33,15 @@ def patch(src):
         src = new
 
     sub(r"(namespace \{\n)", r"\1__device__ unsigned long long g_stamps[8 * 65536];\n")
+    if twice:  # diagnostic: the integration runs twice; stamp 7 = end of the first (cold i-cache) run
+        sub(r"(    const bool event = physics_step<MODEL, INTEG>\(P, a, y0, y1\);\n)",
+            r"    {\n        float yx[NS], yb[NS], z = 0.0f;\n        asm volatile(\"\" : \"+v\"(z));\n"
+            r"        for (int j = 0; j < NS; ++j) yb[j] = y0[j] + z;\n"
+            r"        const bool ex = physics_step<MODEL, INTEG>(P, a, yb, yx);\n"
+            r"        asm volatile(\"; first\" ::\"v\"(yx[0]), \"v\"(yx[13]), \"v\"((float)ex));\n    }\n"
+            r"    const unsigned long long stx = __builtin_amdgcn_s_memrealtime();\n\1"
+            r"    asm volatile(\"; second\" ::\"v\"(y1[0]), \"v\"(y1[13]));\n"
+            r"    const unsigned long long sty = __builtin_amdgcn_s_memrealtime();\n")
     sub(r"(    const bool valid = i < n;\n)",
         r"\1    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();\n")
     sub(r"(    const CounterLayout CL\(P\);\n)",
@@ -57,15 +66,17 @@ def patch(src):
         r"        unsigned long long* g = g_stamps + 8 * wave_idx;\n"
         r"        g[0] = st0; g[1] = st1; g[2] = st2; g[3] = st3; g[4] = st4; g[5] = st5; g[6] = st6; g[7] = st7;\n"
         r"    }\n")
+    if twice:
+        src = src.replace("g[4] = st4;", "g[4] = sty;").replace("g[7] = st7;", "g[7] = stx;")
     sub(r"(extern \"C\" \{\n)", r"\1void* rr_diag_stamps() { void* p = nullptr; "
         r"(void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)); return p; }\n")
     return src
 
 
-def build():
+def build(twice=False):
     from rl_rocket_amd import build as b
 
-    src = patch(open(b.SRC).read())
+    src = patch(open(b.SRC).read(), twice)
     tmp = os.path.join(ROOT, ".ab", "stamp_src")
     os.makedirs(tmp, exist_ok=True)
     for f in [os.path.basename(p) for p in b.DEPS]:
@@ -80,7 +91,7 @@ def build():
     print(OUT)
 
 
-def run(k, n):
+def run(k, n, twice=False):
     os.environ["RR_LIB_PATH"] = OUT
     import numpy as np
     import torch
@@ -127,6 +138,11 @@ def run(k, n):
     t = (st[:, :7] - st[:, 0].min()) * 10  # ns
     has_done = st[:, 7] > 0
     q = lambda a: {p: float(np.percentile(a, p)) for p in (0, 50, 90, 99, 100)}  # noqa: E731
+    if twice:  # slot 7 = end of the first integration, slot 4 = end of the second
+        print(json.dumps({"k": k, "n": n, "twice": True,
+                          "ns_first_integration": q((st[:, 7] - st[:, 1]) * 10),
+                          "ns_second_integration": q((st[:, 4] - st[:, 7]) * 10)}, indent=1))
+        return
     print(json.dumps({
         "k": k, "n": n, "event_us_per_launch": e0.elapsed_time(e1) * 1e3 / k,
         "ns_start": q(t[:, 0]), "ns_loads_landed": q(t[:, 1] - t[:, 0]), "ns_compute": q(t[:, 2] - t[:, 1]),
@@ -146,8 +162,9 @@ def main():
     ap.add_argument("what", choices=["build", "run"])
     ap.add_argument("--k", type=int, default=20)
     ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--twice", action="store_true", help="diagnostic: integrate twice (cold vs warm i-cache)")
     a = ap.parse_args()
-    build() if a.what == "build" else run(a.k, a.n)
+    build(a.twice) if a.what == "build" else run(a.k, a.n, a.twice)
 
 
 if __name__ == "__main__":
