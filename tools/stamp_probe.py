@@ -33,14 +33,20 @@ def patch(src, twice=False):
         src = new
 
     sub(r"(namespace \{\n)", r"\1__device__ unsigned long long g_stamps[8 * 65536];\n")
-    if twice:  # diagnostic: the integration runs twice; stamp 7 = end of the first (cold i-cache) run
+    if twice:  # diagnostic: the same integration code runs twice (a loop, so the same instruction
+        # addresses) after every load has landed; stamp 7 = end of pass 0 (cold i-cache), 4 = end of pass 1
         sub(r"(    const bool event = physics_step<MODEL, INTEG>\(P, a, y0, y1\);\n)",
-            r"    {\n        float yx[NS], yb[NS], z = 0.0f;\n        asm volatile(\"\" : \"+v\"(z));\n"
+            r"    asm volatile(\"; all loads\" ::\"v\"(y0[1]), \"v\"(y0[2]), \"v\"(y0[3]), \"v\"(y0[4]), "
+            r"\"v\"(y0[5]), \"v\"(y0[7]), \"v\"(y0[8]), \"v\"(y0[9]), \"v\"(y0[10]), \"v\"(y0[11]), "
+            r"\"v\"(y0[12]), \"v\"(a[1]));\n"
+            r"    const unsigned long long stw = __builtin_amdgcn_s_memrealtime();\n"
+            r"    unsigned long long stx = 0;\n    bool event = false;\n"
+            r"#pragma unroll 1\n    for (int pass = 0; pass < 2; ++pass) {\n"
+            r"        float z = 0.0f;\n        asm volatile(\"\" : \"+v\"(z));\n        float yb[NS];\n"
             r"        for (int j = 0; j < NS; ++j) yb[j] = y0[j] + z;\n"
-            r"        const bool ex = physics_step<MODEL, INTEG>(P, a, yb, yx);\n"
-            r"        asm volatile(\"; first\" ::\"v\"(yx[0]), \"v\"(yx[13]), \"v\"((float)ex));\n    }\n"
-            r"    const unsigned long long stx = __builtin_amdgcn_s_memrealtime();\n\1"
-            r"    asm volatile(\"; second\" ::\"v\"(y1[0]), \"v\"(y1[13]));\n"
+            r"        event = physics_step<MODEL, INTEG>(P, a, yb, y1);\n"
+            r"        asm volatile(\"; pass\" ::\"v\"(y1[0]), \"v\"(y1[13]));\n"
+            r"        if (pass == 0) stx = __builtin_amdgcn_s_memrealtime();\n    }\n"
             r"    const unsigned long long sty = __builtin_amdgcn_s_memrealtime();\n")
     sub(r"(    const bool valid = i < n;\n)",
         r"\1    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();\n")
@@ -68,6 +74,7 @@ def patch(src, twice=False):
         r"    }\n")
     if twice:
         src = src.replace("g[4] = st4;", "g[4] = sty;").replace("g[7] = st7;", "g[7] = stx;")
+        src = src.replace("g[1] = st1;", "g[1] = stw;")
     sub(r"(extern \"C\" \{\n)", r"\1void* rr_diag_stamps() { void* p = nullptr; "
         r"(void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)); return p; }\n")
     return src
