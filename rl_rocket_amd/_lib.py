@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
@@ -94,6 +94,7 @@ SIGNATURES = {
     "rr_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "rr_step_rows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "rr_step_repeat": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, _P]),
+    "rr_step_repeat_timed": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rr_set_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_get_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_set_state64": (ctypes.c_int, [_P, _P, _P, _P, _P]),

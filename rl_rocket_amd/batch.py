@@ -122,19 +122,26 @@ class RocketBatch:
                                          self._stream()), "rr_step_rows")
         return rows
 
-    def step_repeat(self, actions, n_steps):
+    def step_repeat(self, actions, n_steps, events=None):
         """`n_steps` consecutive steps, step t taking action batch t % len(actions) of the device
-        tensor `actions` [B][N][action_dim] (rr_step_repeat: one host call). Returns the output
-        tensors of the last step."""
+        tensor `actions` [B][N][action_dim] (rr_step_repeat: one host call, direct dispatch).
+        `events` = (start, end) torch.cuda.Event pair recorded right before the first and right
+        after the last launch (rr_step_repeat_timed). Returns the output tensors of the last step."""
         t = self.torch
         if not isinstance(actions, t.Tensor) or actions.device != self.device or actions.dtype != t.float32:
             raise TypeError("actions must be a float32 tensor on %s" % self.device)
         shape = (self.action_dim, self.num_envs) if self.action_soa else (self.num_envs, self.action_dim)
         actions = actions.reshape((-1,) + shape).contiguous()
         self._last_action = actions
-        _lib.check(self.lib.rr_step_repeat(self._h, _ptr(actions), actions.shape[0], int(n_steps), _ptr(self.obs),
-                                           _ptr(self.reward), _ptr(self.done), _ptr(self.truncated), _ptr(self.terms),
-                                           self._stream()), "rr_step_repeat")
+        args = (self._h, _ptr(actions), actions.shape[0], int(n_steps), _ptr(self.obs), _ptr(self.reward),
+                _ptr(self.done), _ptr(self.truncated), _ptr(self.terms), self._stream())
+        if events is None:
+            _lib.check(self.lib.rr_step_repeat(*args), "rr_step_repeat")
+        else:
+            ev = [ctypes.c_void_p(e.cuda_event) for e in events]
+            if not all(e.value for e in ev):
+                raise ValueError("step_repeat: the events must exist (record them once before timing)")
+            _lib.check(self.lib.rr_step_repeat_timed(*args, ev[0], ev[1]), "rr_step_repeat_timed")
         return self.obs, self.reward, self.done, self.truncated
 
     def set_state(self, state_soa, v0=None, elapsed=None):

@@ -220,3 +220,64 @@ def test_checkpoint_restore_is_bitwise():
     b.set_state(ck["state"], v0=ck["v0"])
     el, ep = b.split_counter(b.checkpoint()["counter"])
     assert bool((el == 0).all()) and bool((ep == 123).all())
+
+
+@pytest.mark.parametrize("model,n,soa", [(6, 4096 + 77, False), (6, 20003, False), (6, 131072 + 5, True),
+                                         (3, 20003, True), (3, 4096 + 77, False)])
+def test_step_repeat_direct_launch_is_bitwise_step(model, n, soa):
+    """rr_step_repeat / rr_step_repeat_timed dispatch step_dl_kernel, which reads its parameters
+    and buffer pointers from the device launch block: bitwise the same outputs, terminal rows,
+    Monitor returns and state as one rr_step per step, across a re-seed (the block is rewritten
+    in stream order), with the timing events recorded, and under stream capture (by-value
+    kernel recorded)."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    kw = _env6() if model == 6 else {}
+    mk = lambda: RocketBatch(n, model=model, device="cuda:0", max_episode_steps=30, compute_terms=True,  # noqa: E731
+                             action_soa=soa, **kw)
+    a, b = mk(), mk()
+    a.reset()
+    b.reset()
+    pool = torch.rand((3, n, a.action_dim), device="cuda:0", generator=torch.Generator("cuda:0").manual_seed(5)) * 2 - 1
+    if soa:
+        pool = pool.transpose(1, 2).contiguous()
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    for e in ev:
+        e.record()
+    resets = 0
+    for chunk, seed in ((7, None), (25, 99), (1, None), (40, None)):
+        if seed is not None:
+            a.seed(seed)
+            b.seed(seed)
+        for t in range(chunk):
+            a.step(pool[t % 3])
+            resets += int(a.done.sum())
+        b.step_repeat(pool, chunk, events=ev)
+        torch.cuda.synchronize()
+        assert ev[0].elapsed_time(ev[1]) > 0.0
+        for x, y in ((a.obs, b.obs), (a.reward, b.reward), (a.done, b.done), (a.truncated, b.truncated),
+                     (a.terms, b.terms)):
+            assert torch.equal(x, y)
+        for x, y in zip(a.get_state(), b.get_state()):
+            assert torch.equal(x, y)
+        ca, cb = a.checkpoint(), b.checkpoint()
+        for k in ca:
+            assert torch.equal(ca[k], cb[k]), k
+    assert resets > n // 2
+    # captured: the graph records the by-value kernel; replays match eager steps
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            b.step_repeat(pool, 3)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(2):
+        for t in range(3):
+            a.step(pool[t])
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward)
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
