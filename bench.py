@@ -26,6 +26,10 @@ sys.path.insert(0, ROOT)
 BYTES_PER_STEP = {6: 56 + 12 + 4 + 56 + 56 + 4 + 1, 3: 28 + 8 + 4 + 28 + 28 + 4 + 1}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 POOL = 8
+# --launch auto: direct launches (rr_step_repeat_timed) below this many timed steps, hipGraph
+# replays from here on (crossover of the ~8 us per-replay preamble against ~0.3 us per direct
+# launch, measured at N = 65536: DESIGN.md section 5)
+AUTO_LOOP_MAX_K = 32
 
 
 def parse():
@@ -41,9 +45,12 @@ def parse():
                     help="the drop-in default (RocketVecEnv monitor=True): Monitor running return kept per env "
                          "(read + written every step, +8 B per env-step); the headline runs without it")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--launch", default="graph", choices=["graph", "loop"],
-                    help="graph: K launches replayed from hipGraphs; loop: one rr_step_repeat call (K launches "
-                         "issued back to back from C, action batch t % 8 of the resident pool)")
+    ap.add_argument("--launch", default="auto", choices=["auto", "graph", "loop"],
+                    help="graph: K launches replayed from hipGraphs; loop: one rr_step_repeat_timed call (K direct "
+                         "launches issued back to back from C, action batch t mod 8 of the resident pool, the HIP "
+                         "events recorded by the call around them); auto: loop for K < %d, else graph (a graph "
+                         "replay carries a fixed ~8 us preamble on the GPU timeline, a direct launch ~0.3 us more "
+                         "than a graph-captured one: DESIGN.md section 5)" % AUTO_LOOP_MAX_K)
     ap.add_argument("--graph-steps", type=int, default=1024,
                     help="env steps captured per hipGraph (each replay costs a fixed ~15-20 us on the GPU "
                          "timeline: 64 -> 4.34 us/step, 256 -> 4.25, 1024 -> 4.18 at N=65536)")
@@ -310,14 +317,17 @@ def main():
             env.step(pool[k % POOL])
 
     stream = torch.cuda.current_stream(dev)
-    use_loop = args.launch == "loop" and not args.allgather
+    launch = args.launch
+    if launch == "auto":
+        launch = "loop" if args.steps < AUTO_LOOP_MAX_K and not args.allgather else "graph"
+    use_loop = launch == "loop" and not args.allgather
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if use_loop:
         # the same call as the timed region (its launch block is written once, here), and the
         # two timing events created so that the C call can record them
-        env.step_repeat(pool, args.warmup)
         ev0.record(stream)
         ev1.record(stream)
+        env.step_repeat(pool, args.warmup, events=(ev0, ev1))
     else:
         for k in range(args.warmup):
             one(k)
@@ -325,7 +335,7 @@ def main():
 
     # ---- timed region: exactly K steps (hipGraph replays) ----
     # step + all_gather graphs need a capturable collective (RCCL); gloo is a host path
-    use_graph = not args.no_graph and args.launch == "graph" and not (gather is not None and backend == "gloo")
+    use_graph = not args.no_graph and launch == "graph" and not (gather is not None and backend == "gloo")
     # exactly K steps: K // gs replays of a gs-launch graph (gs balanced so that K = 2000 is
     # 2 x 1000, not 1024 + 976) plus one graph of the K % gs remainder launches
     K = args.steps
@@ -356,11 +366,13 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    if use_loop:
+        fn, fargs = env.step_repeat_call(pool, K, (ev0, ev1))
     t0 = time.perf_counter()
     if use_loop:
         # K direct launches from one C call, which records the two HIP events on the launch
         # stream right before the first and right after the last launch
-        env.step_repeat(pool, K, events=(ev0, ev1))
+        rc = fn(*fargs)
     else:
         ev0.record(stream)  # HIP events on the stream the step kernels are launched on
         if use_graph:
@@ -376,6 +388,9 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if use_loop:
+        from rl_rocket_amd import _lib
+        _lib.check(rc, "rr_step_repeat_timed")
     # device time per launch over the timed region (kernel + inter-kernel gap inside the
     # graph: an upper bound on the kernel's own duration, so `achieved` is conservative).
     # (Events recorded with hipEventReleaseToDevice instead of torch's system-scope release
@@ -414,7 +429,7 @@ def main():
                                   "no data-path collective") + (", Monitor returns" if args.monitor else ""),
                    "envs_per_gpu": n, "global_envs": n * world, "integrator": args.integrator,
                    "graph_steps": gs if use_graph else 0, "launch": "graph" if use_graph else
-                   ("rr_step_repeat" if use_loop else "rr_step per step"),
+                   ("direct: rr_step_repeat_timed" if use_loop else "rr_step per step"),
                    "parallelism": "env-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "B/launch",
@@ -422,6 +437,9 @@ def main():
                      "kernel": "step_kernel<%d,%s>" % (model, args.integrator.upper()),
                      "kernel_us": kern_ms * 1e3,
                      "timing": "HIP events on the launch stream around the K launches of the timed region" +
+                               (" (recorded by rr_step_repeat_timed itself; the first 4 launches are queued "
+                                "behind a host-released gate kernel so the host's submission stays ahead)"
+                                if use_loop else " (around the hipGraph replays)") +
                                (" (each step = rr_step_rows + the RCCL all_gather, so kernel_us includes the "
                                 "collective)" if gather is not None else ""),
                      "bytes_per_launch": bytes_launch,

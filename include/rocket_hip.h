@@ -168,15 +168,13 @@ int rr_step_rows(rr_env* e, const float* action, float* rows, uint8_t* truncated
  * last step. */
 int rr_step_repeat(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs, float* reward,
                    uint8_t* done, uint8_t* truncated, float* terms, void* stream);
-/* rr_step_repeat with two optional hipEvent_t (as void*, NULL = none) recorded on `stream`
- * right before the first and right after the last step launch, so that an event-timed region
- * holds exactly the n_steps launches (bench.py --launch loop). Both calls dispatch directly:
- * outside stream capture the RK4 / Euler steps read their parameters and buffer pointers from
- * a device-resident launch block, rewritten in stream order (one tiny kernel, before
- * ev_start) only when the buffers, parameters or seed changed since the previous call; a
- * directly dispatched kernel's argument segment is not held by the scalar cache (DESIGN.md
- * §3). Calls with different buffers on different streams must be ordered by the caller.
- * Under capture the by-value rr_step kernel is recorded. (ABI v6) */
+/* rr_step_repeat with a pair of hipEvent_t (as void*; both or neither) recorded on `stream`
+ * right before the first and right after the last of the n_steps launches, for an event-timed
+ * region that holds exactly those launches (bench.py --launch loop). The stream is held behind
+ * a one-wave gate kernel (time-bounded, 1 s) that the call releases once the first 2 launches
+ * are submitted: the host (~3 us per direct launch) then stays ahead of the GPU (~4.4 us per
+ * step at N = 65536), so the region measures back-to-back launches rather than the host's
+ * submission pace. Not capturable. (ABI v6) */
 int rr_step_repeat_timed(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs,
                          float* reward, uint8_t* done, uint8_t* truncated, float* terms, void* stream,
                          void* ev_start, void* ev_end);

@@ -122,6 +122,23 @@ class RocketBatch:
                                          self._stream()), "rr_step_rows")
         return rows
 
+    def step_repeat_call(self, actions, n_steps, events):
+        """(function, arguments) of the rr_step_repeat_timed call that step_repeat(actions, n_steps,
+        events) makes, prepared once (bench.py times the bare C call)."""
+        t = self.torch
+        if not isinstance(actions, t.Tensor) or actions.device != self.device or actions.dtype != t.float32:
+            raise TypeError("actions must be a float32 tensor on %s" % self.device)
+        shape = (self.action_dim, self.num_envs) if self.action_soa else (self.num_envs, self.action_dim)
+        if not actions.is_contiguous() or tuple(actions.shape[1:]) != shape:
+            raise ValueError("actions must be a contiguous [B]%s tensor" % (list(shape),))
+        ev = [ctypes.c_void_p(e.cuda_event) for e in events]
+        if not all(e.value for e in ev):
+            raise ValueError("step_repeat: the events must exist (record them once before timing)")
+        self._last_action = actions
+        return self.lib.rr_step_repeat_timed, (self._h, _ptr(actions), actions.shape[0], int(n_steps), _ptr(self.obs),
+                                               _ptr(self.reward), _ptr(self.done), _ptr(self.truncated),
+                                               _ptr(self.terms), self._stream(), ev[0], ev[1])
+
     def step_repeat(self, actions, n_steps, events=None):
         """`n_steps` consecutive steps, step t taking action batch t % len(actions) of the device
         tensor `actions` [B][N][action_dim] (rr_step_repeat: one host call, direct dispatch).

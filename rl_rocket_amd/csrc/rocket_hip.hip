@@ -1052,14 +1052,10 @@ __device__ __forceinline__ void store_outputs(const StepIO& io, uint32_t i, uint
 // ROWS (rr_step_rows): obs, reward and done leave as ONE row of NS + 2 fp32 per env
 // (obs[NS], reward, done as 0 / 1) through the same LDS tile, e.g. straight into the send
 // buffer of the multi-GPU all-gather (rl_rocket_amd.dist.ShardGather).
-// The body takes its parameter blocks by reference: step_kernel passes its kernel arguments
-// (graph-captured launches: the captured kernarg segment is read through the scalar cache),
-// step_dl_kernel a device-resident StepLaunch block (direct dispatch, see there). PH is what
-// the helper role reads: the device copy B.kp, or the launch block's own P.
 template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB, bool ROWS>
-__device__ __forceinline__ void step_body(float* __restrict__ state, const float* __restrict__ action,
-                                          uint32_t n_envs, uint32_t mode, const KParams& P, const KParams& PH,
-                                          const Bufs& B, const StepIO& io)
+__global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR void step_kernel(
+    float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
+    const Bufs B, const StepIO io)
 {
     constexpr int NS = Dims<MODEL>::NS, NA = Dims<MODEL>::NA, NT = Dims<MODEL>::NT, EV = Dims<MODEL>::EV;
     constexpr int OW = ROWS ? NS + 2 : NS;  // floats per output row
@@ -1079,7 +1075,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ state, const float
             // the helper role reads its parameters through the device copy (B.kp): kernel-argument
             // values it used were loaded in the kernel's entry block and kept live into the main
             // role, where SGPRs are the scarce resource
-            const KParams& P = PH;
+            const KParams& P = *B.kp;
             const uint32_t k = wv - WPB;  // the main wave this helper serves
             const uint32_t base = (blockIdx.x * WPB + k) * kWave;
             const uint32_t ih = min(base + lane, n - 1);
@@ -1201,44 +1197,6 @@ __device__ __forceinline__ void step_body(float* __restrict__ state, const float
         store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
                                   io.obs_vec_ok);
     }
-}
-
-template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB, bool ROWS>
-__global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR void step_kernel(
-    float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
-    const Bufs B, const StepIO io)
-{
-    step_body<MODEL, INTEG, ASOA, HELP, WPB, ROWS>(state, action, n_envs, mode, P, *B.kp, B, io);
-}
-
-// Everything a step launch reads besides its four leading (preloaded) arguments, resident in
-// device memory (rr_env.d_launch, written in stream order by set_launch_kernel when it changes).
-struct StepLaunch {
-    KParams P;
-    Bufs B;
-    StepIO io;
-};
-
-__global__ __launch_bounds__(64) void set_launch_kernel(const StepLaunch L, StepLaunch* __restrict__ dst)
-{
-    static_assert(sizeof(StepLaunch) % 4 == 0, "StepLaunch copied as 32-bit words");
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(&L);
-    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-    for (uint32_t w = threadIdx.x; w < sizeof(StepLaunch) / 4; w += 64) d[w] = s[w];
-}
-
-// Direct-dispatch form of the step (rr_step_repeat): the kernel-argument segment of a directly
-// dispatched kernel is not held by the scalar cache (every dependent s_load of it took 52-67 ns
-// against 31-35 ns for a graph-captured segment or device memory, tools/kernarg_latency.hip,
-// profiles/r02/r02y/kernarg_latency.json), and the step re-reads its parameters and output
-// pointers after the integration. Here only the pointer to the launch block comes from the
-// kernarg segment; the block itself is ordinary device memory read through the scalar cache.
-template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB>
-__global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR void step_dl_kernel(
-    float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode,
-    const StepLaunch* __restrict__ L)
-{
-    step_body<MODEL, INTEG, ASOA, HELP, WPB, false>(state, action, n_envs, mode, L->P, L->P, L->B, L->io);
 }
 
 template <int MODEL>
@@ -1473,10 +1431,8 @@ struct rr_env {
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
     KParams* d_kp;      // device copy of kp (Bufs.kp)
-    StepLaunch* d_launch;  // device launch block of step_dl_kernel (rr_step_repeat)
-    StepLaunch h_launch;   // what d_launch holds (valid once launch_set)
-    bool launch_set;
-    bool repeat_dl;        // rr_step_repeat dispatches step_dl_kernel (RR_REPEAT_DL=0: by-value kernel, A/B)
+    uint32_t* gate;     // host-pinned word releasing gate_kernel (rr_step_repeat_timed), lazily allocated
+    uint32_t gate_gen;
     int32_t* g_idx;     // rr_fetch_done scratch
     float* g_obs;
     float* g_ret;
@@ -1554,8 +1510,6 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         // test / A-B override of the helper-wave threshold: RR_HELP_MAX_N=<n> in the environment
         const char* hv = std::getenv("RR_HELP_MAX_N");
         e->help_max_n = hv ? std::strtoll(hv, nullptr, 10) : (int64_t)RR_HELP_MAX_N;
-        const char* dv = std::getenv("RR_REPEAT_DL");
-        e->repeat_dl = !(dv && dv[0] == '0');
     }
     DeviceGuard g(device);
     struct A {
@@ -1597,7 +1551,6 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->kp.id_off = env_id_offset;
     {
         hipError_t err = hipMalloc((void**)&e->d_kp, sizeof(KParams));
-        if (err == hipSuccess) err = hipMalloc((void**)&e->d_launch, sizeof(StepLaunch));
         if (err != hipSuccess) {
             rr_destroy(e);
             return hip_fail(err, "rr_create: hipMalloc (params)");
@@ -1620,10 +1573,11 @@ int rr_destroy(rr_env* e)
 {
     if (!e) return RR_OK;
     DeviceGuard g(e->device);
-    void* ptrs[] = {e->state, e->state64, e->d_kp, e->d_launch, e->done_bits,
+    void* ptrs[] = {e->state, e->state64, e->d_kp, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
+    if (e->gate) (void)hipHostFree(e->gate);
     delete e;
     return RR_OK;
 }
@@ -1660,6 +1614,20 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
 }  // extern "C"
 
 namespace {
+constexpr int64_t kGateQueued = 2;                  // launches queued behind the gate before its release
+constexpr uint64_t kGateMaxTicks = 100000000ull;    // 1 s of the 100 MHz realtime clock
+
+// One wave holds the stream until the host-written word reaches `gen` (rr_step_repeat_timed),
+// or `ticks` of the 100 MHz realtime clock pass: every path exits.
+__global__ __launch_bounds__(64) void gate_kernel(const uint32_t* word, uint32_t gen, uint64_t ticks)
+{
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 // one step launch (rr_step / rr_step_repeat; arguments checked by the caller)
 template <bool ROWS>
 int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
@@ -1728,51 +1696,6 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     e->steps++;
     return RR_OK;
 }
-
-// one direct-dispatch step launch from the device launch block (rr_step_repeat; RK4 / Euler)
-int launch_step_dl(rr_env* e, const float* action, hipStream_t s)
-{
-    const bool m6 = e->p.model == RR_MODEL_6DOF;
-    const bool euler = e->p.integrator == RR_INT_EULER;
-    const dim3 grid(grid_of(e->n)), block(kBlock);
-    const uint32_t nn = (uint32_t)e->n;
-    const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
-    const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
-    const bool soa = e->p.flags & RR_FLAG_ACTION_SOA;
-    const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;
-    const bool narrow = e->n <= RR_NARROW_MAX_N;
-    const StepLaunch* L = e->d_launch;
-#define RR_LAUNCH_DL(M, I, A)                                                                                       \
-    do {                                                                                                             \
-        if (help && narrow)                                                                                          \
-            hipLaunchKernelGGL((step_dl_kernel<M, I, A, true, 1>), dim3((unsigned)((e->n + kWave - 1) / kWave)),    \
-                               dim3(2 * kWave), 0, s, e->state, action, nn, mode, L);                                \
-        else if (help)                                                                                               \
-            hipLaunchKernelGGL((step_dl_kernel<M, I, A, true, kWavesPerBlock>), grid, dim3(2 * kBlock), 0, s,        \
-                               e->state, action, nn, mode, L);                                                       \
-        else                                                                                                         \
-            hipLaunchKernelGGL((step_dl_kernel<M, I, A, false, kWavesPerBlock>), grid, block, 0, s, e->state,        \
-                               action, nn, mode, L);                                                                 \
-    } while (0)
-    if (m6 && !euler) {
-        if (soa) RR_LAUNCH_DL(6, RR_INT_RK4, true);
-        else RR_LAUNCH_DL(6, RR_INT_RK4, false);
-    } else if (m6) {
-        if (soa) RR_LAUNCH_DL(6, RR_INT_EULER, true);
-        else RR_LAUNCH_DL(6, RR_INT_EULER, false);
-    } else if (!euler) {
-        if (soa) RR_LAUNCH_DL(3, RR_INT_RK4, true);
-        else RR_LAUNCH_DL(3, RR_INT_RK4, false);
-    } else {
-        if (soa) RR_LAUNCH_DL(3, RR_INT_EULER, true);
-        else RR_LAUNCH_DL(3, RR_INT_EULER, false);
-    }
-#undef RR_LAUNCH_DL
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return hip_fail(err, "rr_step_repeat: launch");
-    e->steps++;
-    return RR_OK;
-}
 }  // namespace
 
 extern "C" {
@@ -1808,46 +1731,54 @@ int rr_step_repeat_timed(rr_env* e, const float* actions, int64_t n_batches, int
     if (!e) return fail(RR_EINVAL, "rr_step_repeat: null handle");
     if (!actions || !obs || !reward || !done) return fail(RR_EINVAL, "rr_step_repeat: actions/obs/reward/done required");
     if (n_batches <= 0 || n_steps < 0) return fail(RR_EINVAL, "rr_step_repeat: n_batches must be >= 1, n_steps >= 0");
+    if (!ev_start != !ev_end) return fail(RR_EINVAL, "rr_step_repeat_timed: give both events or neither");
     hipStream_t s = (hipStream_t)stream;
-    // direct dispatch reads the launch block from device memory (step_dl_kernel); under stream
-    // capture the by-value kernel is recorded instead (a replay must not depend on d_launch)
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cap) != hipSuccess) cap = hipStreamCaptureStatusNone;
-    const bool dl = e->repeat_dl && cap == hipStreamCaptureStatusNone && e->p.integrator != RR_INT_DOPRI5;
-    if (dl) {
-        StepLaunch L;
-        std::memset(&L, 0, sizeof(L));
-        std::memcpy(&L.P, &e->kp, sizeof(KParams));
-        L.B = bufs_of(e);
-        L.io.obs = obs;
-        L.io.reward = reward;
-        L.io.done = done;
-        L.io.truncated = truncated;
-        L.io.terms = terms;
-        L.io.obs_vec_ok = ((uintptr_t)obs & 15u) == 0;
-        if (!e->launch_set || std::memcmp(&L, &e->h_launch, sizeof(L)) != 0) {
-            hipLaunchKernelGGL(set_launch_kernel, dim3(1), dim3(64), 0, s, L, e->d_launch);
-            hipError_t err = hipGetLastError();
-            if (err != hipSuccess) return hip_fail(err, "rr_step_repeat: launch block");
-            std::memcpy(&e->h_launch, &L, sizeof(L));
-            e->launch_set = true;
+    hipError_t err = hipSuccess;
+    // Timed form: the stream is held by gate_kernel until the first kGateQueued launches of the
+    // region have been submitted (2: the wall clock waits for as few as possible). A direct launch costs ~3 us of host time against ~4.4 us of
+    // GPU time per step at N = 65536, so from there on the host stays ahead and the events
+    // bracket back-to-back launches on the GPU timeline (without the gate the GPU idles while
+    // the first launch is submitted, and a stall of the submitting thread early in a short
+    // region lands inside it); released early so the wall clock does not wait for all K.
+    const bool gate = ev_start != nullptr;
+    if (ev_start) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        err = hipStreamIsCapturing(s, &cap);
+        if (err != hipSuccess) return hip_fail(err, "rr_step_repeat_timed: stream query");
+        if (cap != hipStreamCaptureStatusNone) return fail(RR_EINVAL, "rr_step_repeat_timed: not capturable");
+    }
+    if (gate) {
+        if (!e->gate) {
+            err = hipHostMalloc((void**)&e->gate, 64, hipHostMallocCoherent);
+            if (err != hipSuccess) {
+                e->gate = nullptr;
+                return hip_fail(err, "rr_step_repeat_timed: gate word");
+            }
+            __atomic_store_n(e->gate, 0u, __ATOMIC_SEQ_CST);
+            e->gate_gen = 0;
+        }
+        ++e->gate_gen;
+        hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)e->gate, e->gate_gen,
+                           (uint64_t)kGateMaxTicks);
+        err = hipGetLastError();
+        if (err != hipSuccess) return hip_fail(err, "rr_step_repeat_timed: gate launch");
+    }
+    int rc = RR_OK;
+    if (ev_start && (err = hipEventRecord((hipEvent_t)ev_start, s)) != hipSuccess)
+        rc = hip_fail(err, "rr_step_repeat_timed: start event");
+    const int64_t batch = e->n * e->na;
+    bool held = gate;
+    for (int64_t t = 0; t < n_steps && rc == RR_OK; ++t) {
+        rc = launch_step<false>(e, actions + (t % n_batches) * batch, obs, reward, done, truncated, terms, stream);
+        if (held && t + 1 >= kGateQueued) {
+            __atomic_store_n(e->gate, e->gate_gen, __ATOMIC_SEQ_CST);
+            held = false;
         }
     }
-    if (ev_start) {
-        hipError_t err = hipEventRecord((hipEvent_t)ev_start, s);
-        if (err != hipSuccess) return hip_fail(err, "rr_step_repeat: start event");
-    }
-    const int64_t batch = e->n * e->na;
-    for (int64_t t = 0; t < n_steps; ++t) {
-        const float* a = actions + (t % n_batches) * batch;
-        const int rc = dl ? launch_step_dl(e, a, s) : launch_step<false>(e, a, obs, reward, done, truncated, terms, stream);
-        if (rc != RR_OK) return rc;
-    }
-    if (ev_end) {
-        hipError_t err = hipEventRecord((hipEvent_t)ev_end, s);
-        if (err != hipSuccess) return hip_fail(err, "rr_step_repeat: end event");
-    }
-    return RR_OK;
+    if (rc == RR_OK && ev_end && (err = hipEventRecord((hipEvent_t)ev_end, s)) != hipSuccess)
+        rc = hip_fail(err, "rr_step_repeat_timed: end event");
+    if (held) __atomic_store_n(e->gate, e->gate_gen, __ATOMIC_SEQ_CST);  // released on every path
+    return rc;
 }
 
 namespace {

@@ -222,14 +222,13 @@ def test_checkpoint_restore_is_bitwise():
     assert bool((el == 0).all()) and bool((ep == 123).all())
 
 
-@pytest.mark.parametrize("model,n,soa", [(6, 4096 + 77, False), (6, 20003, False), (6, 131072 + 5, True),
+@pytest.mark.parametrize("model,n,soa", [(6, 4096 + 77, False), (6, 20003, False), (6, 131072 + 5, True), (6, 65536, False),
                                          (3, 20003, True), (3, 4096 + 77, False)])
 def test_step_repeat_direct_launch_is_bitwise_step(model, n, soa):
-    """rr_step_repeat / rr_step_repeat_timed dispatch step_dl_kernel, which reads its parameters
-    and buffer pointers from the device launch block: bitwise the same outputs, terminal rows,
-    Monitor returns and state as one rr_step per step, across a re-seed (the block is rewritten
-    in stream order), with the timing events recorded, and under stream capture (by-value
-    kernel recorded)."""
+    """rr_step_repeat_timed (K direct launches queued behind the host-released gate kernel, two
+    timing events around them) and rr_step_repeat under stream capture: bitwise the same
+    outputs, terminal rows, Monitor returns, counter words and state as one rr_step per step,
+    across a re-seed."""
     import torch
     from rl_rocket_amd.batch import RocketBatch
 

@@ -24,9 +24,13 @@ if [ "${TESTS:-1}" = 1 ]; then
   tail -3 "$OUT/pytest_gpu.log"
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 fi
-for i in 1 2 3; do
+for i in 1 2 3 4 5 6; do
   step bench_k20_$i 300 python bench.py --steps 20 --warmup 5 $BENCH_ARGS > "$OUT/bench_k20_$i.json" 2> "$OUT/bench_k20_$i.err"
   cat "$OUT/bench_k20_$i.json"
+done
+# the same protocol on hipGraph replays (the default launch above is direct below K = 32)
+for i in 1 2; do
+  step bench_graph_k20_$i 300 python bench.py --no-cpu-baseline --launch graph --steps 20 --warmup 5 $BENCH_ARGS > "$OUT/bench_graph_k20_$i.json" 2> "$OUT/bench_graph_k20_$i.err"
 done
 step bench_k2000 300 python bench.py --no-cpu-baseline $BENCH_ARGS > "$OUT/bench_k2000.json" 2> "$OUT/bench_k2000.err"
 cat "$OUT/bench_k2000.json"
