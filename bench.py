@@ -437,7 +437,7 @@ def main():
                      "kernel": "step_kernel<%d,%s>" % (model, args.integrator.upper()),
                      "kernel_us": kern_ms * 1e3,
                      "timing": "HIP events on the launch stream around the K launches of the timed region" +
-                               (" (recorded by rr_step_repeat_timed itself; the first 4 launches are queued "
+                               (" (recorded by rr_step_repeat_timed itself; the first 2 launches are queued "
                                 "behind a host-released gate kernel so the host's submission stays ahead)"
                                 if use_loop else " (around the hipGraph replays)") +
                                (" (each step = rr_step_rows + the RCCL all_gather, so kernel_us includes the "
