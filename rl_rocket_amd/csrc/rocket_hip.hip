@@ -1431,7 +1431,7 @@ struct rr_env {
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
     KParams* d_kp;      // device copy of kp (Bufs.kp)
-    uint32_t* gate;     // host-pinned word releasing gate_kernel (rr_step_repeat_timed), lazily allocated
+    uint32_t* gate;     // host-pinned word releasing gate_kernel (rr_step_repeat_timed)
     uint32_t gate_gen;
     int32_t* g_idx;     // rr_fetch_done scratch
     float* g_obs;
@@ -1551,6 +1551,9 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->kp.id_off = env_id_offset;
     {
         hipError_t err = hipMalloc((void**)&e->d_kp, sizeof(KParams));
+        if (err == hipSuccess) err = hipHostMalloc((void**)&e->gate, 64, hipHostMallocCoherent);
+        if (err == hipSuccess) __atomic_store_n(e->gate, 0u, __ATOMIC_SEQ_CST);
+        else e->gate = nullptr;
         if (err != hipSuccess) {
             rr_destroy(e);
             return hip_fail(err, "rr_create: hipMalloc (params)");
@@ -1748,15 +1751,6 @@ int rr_step_repeat_timed(rr_env* e, const float* actions, int64_t n_batches, int
         if (cap != hipStreamCaptureStatusNone) return fail(RR_EINVAL, "rr_step_repeat_timed: not capturable");
     }
     if (gate) {
-        if (!e->gate) {
-            err = hipHostMalloc((void**)&e->gate, 64, hipHostMallocCoherent);
-            if (err != hipSuccess) {
-                e->gate = nullptr;
-                return hip_fail(err, "rr_step_repeat_timed: gate word");
-            }
-            __atomic_store_n(e->gate, 0u, __ATOMIC_SEQ_CST);
-            e->gate_gen = 0;
-        }
         ++e->gate_gen;
         hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)e->gate, e->gate_gen,
                            (uint64_t)kGateMaxTicks);
