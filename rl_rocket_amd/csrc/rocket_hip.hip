@@ -47,6 +47,14 @@ namespace {
 #ifndef RR_ST_AUX
 #define RR_ST_AUX 0
 #endif
+#ifndef RR_ST_AUX_HELP  // state planes of the helper-wave step kernels (N <= RR_HELP_MAX_N)
+// sc1 (device-scope write-through) where the whole batch's state is a few MB: the end-of-kernel
+// release then has no dirty state lines to write back. A/B at N = 65536 (gpurun_out/q9, q10):
+// direct launches 4.13-4.26 vs 4.34-4.55 us per step, hipGraph replays K = 20 4.39-4.41 vs
+// 4.47-4.48, K = 2000 equal; at N = 524288 (plain kernel, default policy kept) it had cost
+// 10-25 %.
+#define RR_ST_AUX_HELP 16
+#endif
 #ifndef RR_OUT_AUX  // caller-owned outputs (obs, reward, done, truncated)
 // sc1 = device-scope write-through: the outputs leave L2 while the kernel runs instead of
 // in the end-of-kernel writeback (A/B at N = 65536: 5.49 -> 5.18 us; the same bit on the
@@ -1106,6 +1114,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     // (rr_create), so a single descriptor (4 SGPRs) serves them all via soffset
     const rsrc_t st_r = make_rsrc(state, (uint64_t)(NS + 3) * plane);
     const uint32_t v0_off = NS * plane, cw_off = (NS + 1) * plane, ret_off = (NS + 2) * plane;
+    constexpr int SA = HELP ? RR_ST_AUX_HELP : RR_ST_AUX;  // cache policy of the state-buffer stores
 
     // ---- all loads first (one memory round trip per wave); the counter word first, so the
     // reset candidate below is drawn while the state planes are still in flight ----
@@ -1168,7 +1177,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
                 for (int j = 0; j < NS; ++j) y1[j] = ic_s[j];
                 v0 = ic_v0;
             }
-            bst_f(st_r, v0, vo, v0_off);
+            bst_f<SA>(st_r, v0, vo, v0_off);
             cw = CL.next_episode(cw);
             normalize_obs<NS>(y1, H.inv_norm, o);
             el = 0;
@@ -1179,9 +1188,9 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
 
     if (valid) {
 #pragma unroll
-        for (int j = 0; j < NS; ++j) bst_f(st_r, y1[j], vo, j * plane);
-        if (use_counter) bst_u(st_r, cw, vo, (NS + 1) * plane);
-        if (mode & RR_FLAG_EPISODE_STATS) bst_f(st_r, ret, vo, (NS + 2) * plane);
+        for (int j = 0; j < NS; ++j) bst_f<SA>(st_r, y1[j], vo, j * plane);
+        if (use_counter) bst_u<SA>(st_r, cw, vo, (NS + 1) * plane);
+        if (mode & RR_FLAG_EPISODE_STATS) bst_f<SA>(st_r, ret, vo, (NS + 2) * plane);
         store_outputs<NT, !ROWS>(io, i, vo, plane, n, r, done, trunc, t, bv, event);
     }
     const uint32_t nvalid = (n - wave_base) < (uint32_t)kWave ? (n - wave_base) : (uint32_t)kWave;
