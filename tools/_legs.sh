@@ -1,4 +1,4 @@
-O=gpurun_out/r02legs; mkdir -p $O
+O=gpurun_out/${LEGS_TAG:-r02legs}; mkdir -p $O
 run() { local name=$1; shift; timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/$name.json 2> $O/$name.err || { echo "$name failed"; exit 1; }; python -c "
 import json; d=json.loads([l for l in open('$O/$name.json') if l.startswith('{')][-1]); r=d.get('roofline') or {}
 print('$name', round(d['value']/1e9,3), 'G', round(d['ms_per_step']*1e3,3), 'us/step', round(r.get('frac',0) or 0,4))"; }
