@@ -1,20 +1,30 @@
 """Benchmark: 6DOF env-steps/s of the fused HIP step at N envs per GPU (BASELINE.json).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n ENVS_PER_GPU] [--model 6DOF|3DOF]
-                    [--allgather] [--no-graph] [--cpu-seconds S]
+                    [--allgather] [--gather-leg | --no-gather-leg] [--no-sb3-legs] [--cpu-seconds S]
 
 A "step" = one launch of the fused step kernel over all N envs of a GPU: action in,
 RK4 rigid-body step + ground event + reward + done + obs + TimeLimit + auto-reset out.
 Inputs (a pool of 8 pre-generated U(-1,1) action batches, seeded) are resident in HBM
-before the timed region. Multi-GPU: one process per GPU (torchrun), env shards
-[rank*N, (rank+1)*N) with their own RNG streams; no data-path collective unless
---allgather (RCCL all_gather of obs/reward/done after every step).
+before the timed region.
+
+Multi-GPU: one process per GPU. ``--gpus N`` with N > 1 and no WORLD_SIZE in the environment
+starts ``torch.distributed.run`` with N ranks as a CHILD process before anything touches the
+GPU, and exits with its code (it fails loudly when fewer than N GPUs are visible); under
+torchrun (WORLD_SIZE set) ``--gpus`` must equal WORLD_SIZE. Env shards [rank*N, (rank+1)*N)
+with their own reset streams; the headline has no data-path collective. With more than one
+rank the line also carries the step + all_gather leg (obs / reward / done
+rows of every rank gathered each step, RCCL over xGMI), with the world size and backend the
+communicator reports. Rehearsal on one GPU: RR_BENCH_ONE_DEVICE=1 puts every rank on cuda:0
+and RR_BENCH_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU).
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,13 +36,14 @@ sys.path.insert(0, ROOT)
 BYTES_PER_STEP = {6: 56 + 12 + 4 + 56 + 56 + 4 + 1, 3: 28 + 8 + 4 + 28 + 28 + 4 + 1}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 POOL = 8
-# --launch auto: direct launches (rr_step_repeat_timed) below this many timed steps, hipGraph
+# --launch auto: direct launches (tools/libbench_timed.so) below this many timed steps, hipGraph
 # replays from here on (crossover of the ~8 us per-replay preamble against ~0.3 us per direct
 # launch, measured at N = 65536: DESIGN.md section 5)
 AUTO_LOOP_MAX_K = 32
+REFERENCE_PY_STEP = {"6DOF": 569, "3DOF": 3396}  # SURVEY.md §6, survey container, 1 core
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
@@ -40,22 +51,30 @@ def parse():
     ap.add_argument("--n", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--model", default="6DOF")
     ap.add_argument("--integrator", default="rk4")
-    ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--allgather", action="store_true",
+                    help="the headline itself is step rows + all_gather (ShardGather.step) every step")
+    ap.add_argument("--gather-leg", action="store_true",
+                    help="add the step + all_gather leg to the line at any world size (default: only when >1 rank)")
+    ap.add_argument("--no-gather-leg", action="store_true")
     ap.add_argument("--monitor", action="store_true",
                     help="the drop-in default (RocketVecEnv monitor=True): Monitor running return kept per env "
                          "(read + written every step, +8 B per env-step); the headline runs without it")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--launch", default="auto", choices=["auto", "graph", "loop"],
-                    help="graph: K launches replayed from hipGraphs; loop: one rr_step_repeat_timed call (K direct "
-                         "launches issued back to back from C, action batch t mod 8 of the resident pool, the HIP "
-                         "events recorded by the call around them); auto: loop for K < %d, else graph (a graph "
-                         "replay carries a fixed ~8 us preamble on the GPU timeline, a direct launch ~0.3 us more "
-                         "than a graph-captured one: DESIGN.md section 5)" % AUTO_LOOP_MAX_K)
+                    help="graph: K launches replayed from hipGraphs; loop: K direct launches of rr_step issued back "
+                         "to back from C (tools/libbench_timed.so, action batch t mod 8 of the resident pool, the HIP "
+                         "events recorded around them); auto: loop for K < %d, else graph (a graph replay carries "
+                         "a fixed ~8 us preamble on the GPU timeline, a direct launch ~0.3 us more than a "
+                         "graph-captured one: DESIGN.md section 5)" % AUTO_LOOP_MAX_K)
     ap.add_argument("--graph-steps", type=int, default=1024,
                     help="env steps captured per hipGraph (each replay costs a fixed ~15-20 us on the GPU "
                          "timeline: 64 -> 4.34 us/step, 256 -> 4.25, 1024 -> 4.18 at N=65536)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sb3-legs", action="store_true",
+                    help="skip the wall-clock legs through the Python boundary (RocketVecEnv.step with host and "
+                         "device outputs, the single-env gym Rocket6DOF.step)")
+    ap.add_argument("--sb3-steps", type=int, default=100)
     ap.add_argument("--mode", default="step", choices=["step", "rollout"],
                     help="step: the fused env step (headline); rollout: on-device PPO rollout "
                          "collection (MlpPolicy 64x64 forward + sample + env step + buffer), BASELINE configs[4]")
@@ -71,9 +90,187 @@ def parse():
                          "of the whole collect in one rr_rollout_collect launch")
     ap.add_argument("--rollout-torch", action="store_true",
                     help="rollout policy / bootstrap / GAE as PyTorch ops instead of the fused HIP kernels")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------------------------
+# launching N ranks
+# ---------------------------------------------------------------------------------------------
+def launch_plan(gpus, environ):
+    """("run", None): this process is the (only / a torchrun) rank; ("spawn", None): start
+    torchrun with `gpus` ranks as a child; ("error", message) when --gpus contradicts WORLD_SIZE."""
+    if gpus < 1:
+        return "error", "--gpus must be >= 1"
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        return ("spawn", None) if gpus > 1 else ("run", None)
+    if int(ws) != gpus:
+        return "error", ("bench.py --gpus %d but WORLD_SIZE=%s: the rank count and --gpus must agree" % (gpus, ws))
+    return "run", None
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(gpus, argv):
+    """torch.distributed.run with `gpus` ranks, started as a child process before this process
+    has touched the GPU (torch.cuda.device_count() does not initialise it); returns its exit
+    code. Fails loudly when the node shows fewer GPUs than ranks (unless RR_BENCH_ONE_DEVICE=1,
+    the one-GPU rehearsal)."""
+    import torch
+
+    visible = torch.cuda.device_count()
+    one_dev = os.environ.get("RR_BENCH_ONE_DEVICE") == "1"
+    need = 1 if one_dev else gpus
+    if visible < need:
+        print("bench.py --gpus %d needs %d visible GPU(s), found %d (to rehearse N ranks on one GPU set "
+              "RR_BENCH_ONE_DEVICE=1 RR_BENCH_BACKEND=gloo)" % (gpus, need, visible), file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------------------------
+# the timed region
+# ---------------------------------------------------------------------------------------------
+class TimedLoop:
+    """The event-timed direct-launch region: tools/libbench_timed.so (a benchmark-only helper,
+    not the product ABI) issues K rr_step calls of the library behind a host-released gate
+    kernel and records the two HIP events around them (tools/bench_timed.hip)."""
+
+    def __init__(self, env):
+        import ctypes
+
+        from rl_rocket_amd import build as B
+
+        path = B.BENCH_OUT
+        if not os.path.exists(path):
+            raise RuntimeError("%s is not built (python -m rl_rocket_amd.build)" % path)
+        self.ct = ctypes
+        self.lib = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        self.fn = self.lib.bt_step_repeat_timed
+        self.fn.restype = ctypes.c_int
+        self.fn.argtypes = [P, P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, P, P, P, P, P, P, P, P]
+        self.env = env
+        self.rr_step = ctypes.cast(env.lib.rr_step, P)
+
+    def call(self, actions, n_steps, events):
+        """(function, arguments) of one timed call (prepared outside the timed region)."""
+        ct, e = self.ct, self.env
+        P = ct.c_void_p
+        ev = [P(x.cuda_event) for x in events]
+        if not all(x.value for x in ev):
+            raise ValueError("record the events once before timing (they must exist)")
+        ptr = lambda t: P(t.data_ptr()) if t is not None else None  # noqa: E731
+        e._last_action = actions
+        return self.fn, (self.rr_step, e._h, ptr(actions), actions.shape[0], e.num_envs * e.action_dim, int(n_steps),
+                         ptr(e.obs), ptr(e.reward), ptr(e.done), ptr(e.truncated), ptr(e.terms), e._stream(),
+                         ev[0], ev[1])
+
+
+def timed_region(args, env, pool, dev, dist, backend, launch, gather=None):
+    """W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier + synchronize on
+    both sides; returns wall seconds (max over ranks) and the per-launch device time by HIP
+    events on the launch stream."""
+    import torch
+
+    stream = torch.cuda.current_stream(dev)
+    K = args.steps
+
+    def one(k):
+        if gather is not None:
+            # the step writes obs / reward / done straight into the send rows (rr_step_rows),
+            # then ONE all_gather: the global batch on every rank
+            gather.step(env, pool[k % POOL])
+        else:
+            env.step(pool[k % POOL])
+
+    use_loop = launch == "loop" and gather is None
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    loop = TimedLoop(env) if use_loop else None
+    if use_loop:
+        ev0.record(stream)
+        ev1.record(stream)
+        fn, fargs = loop.call(pool, args.warmup, (ev0, ev1))
+        rc = fn(*fargs)
+        if rc != 0:
+            raise RuntimeError("bt_step_repeat_timed (warm-up) failed: %d" % rc)
+    else:
+        for k in range(args.warmup):
+            one(k)
+    torch.cuda.synchronize(dev)
+
+    # step + all_gather graphs need a capturable collective (RCCL); gloo is a host path
+    use_graph = not args.no_graph and launch == "graph" and not (gather is not None and backend == "gloo")
+    # exactly K steps: K // gs replays of a gs-launch graph (gs balanced so that K = 2000 is
+    # 2 x 1000, not 1024 + 976) plus one graph of the K % gs remainder launches
+    gs = max(1, -(-K // max(1, -(-K // max(1, args.graph_steps)))))
+    rem = K % gs
+
+    def capture(n_launch):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(stream)
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for k in range(n_launch):
+                    one(k)
+        stream.wait_stream(s)
+        torch.cuda.synchronize(dev)
+        g.replay()  # warm the graph
+        torch.cuda.synchronize(dev)
+        return g
+
+    if use_graph:
+        graph = capture(gs)
+        graph_rem = capture(rem) if rem else None
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    if use_loop:
+        fn, fargs = loop.call(pool, K, (ev0, ev1))
+    t0 = time.perf_counter()
+    if use_loop:
+        # K direct launches from one C call, which records the two HIP events on the launch
+        # stream right before the first and right after the last launch
+        rc = fn(*fargs)
+    else:
+        ev0.record(stream)  # HIP events on the stream the step kernels are launched on
+        if use_graph:
+            for _ in range(K // gs):
+                graph.replay()
+            if graph_rem is not None:
+                graph_rem.replay()
+        else:
+            for k in range(K):
+                one(k)
+        ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if use_loop and rc != 0:
+        raise RuntimeError("bt_step_repeat_timed failed: %d" % rc)
+    # device time per launch over the timed region (kernel + inter-kernel gap: an upper bound
+    # on the kernel's own duration, so `achieved` is conservative)
+    kern_ms = ev0.elapsed_time(ev1) / K
+    if dist is not None:  # max over ranks of the timed region
+        t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return {"dt": dt, "kern_ms": kern_ms, "use_graph": use_graph, "use_loop": use_loop, "gs": gs}
+
+
+# ---------------------------------------------------------------------------------------------
+# rollout mode (BASELINE configs[4])
+# ---------------------------------------------------------------------------------------------
 def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
     """BASELINE configs[4]: N envs driving an on-device PPO rollout; the whole collect()
     (n_steps x [policy forward, Gaussian sample, env step, timeout bootstrap, buffer
@@ -150,6 +347,9 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
     }
 
 
+# ---------------------------------------------------------------------------------------------
+# CPU baselines (rank 0, N = 1)
+# ---------------------------------------------------------------------------------------------
 def host_cores():
     """CPU threads this process may use (the GPU box shows the whole machine in
     os.cpu_count(); its share is the affinity mask / OMP_NUM_THREADS)."""
@@ -227,37 +427,155 @@ def cpu_baselines(model, seconds, cores):
         head["all_cores"] = cpu_baseline(model, seconds * 0.2, nthreads=cores, n=8192)
     if model == 6:
         head["configs0_3dof_single_env"] = cpu_baseline(3, seconds * 0.2, n=1)
-    head["reference_python_step_survey"] = {"6DOF": 569, "3DOF": 3396, "unit": "env-steps/s", "cores": 1,
-                                            "source": "reference Rocket6DOF / Rocket step(), measured in the survey "
-                                                      "container (SURVEY.md §6, BASELINE.md), not on this box"}
+    head["reference_python_step_survey"] = dict(REFERENCE_PY_STEP, unit="env-steps/s", cores=1,
+                                                source="reference Rocket6DOF / Rocket step(), measured in the survey "
+                                                       "container (SURVEY.md §6, BASELINE.md), not on this box")
     return head
+
+
+# ---------------------------------------------------------------------------------------------
+# wall-clock legs through the Python boundary (what SB3 calls)
+# ---------------------------------------------------------------------------------------------
+def sb3_legs(dev, n, steps):
+    """env-steps/s through the drop-in surface, wall clock, Monitor on, random actions:
+    RocketVecEnv.step with host (numpy) outputs — what SB3's DummyVecEnv.step_wait returns,
+    replacing DummyVecEnv -> Monitor -> TimeLimit -> Rocket6DOF.step (rocket_env.py:690-719) — and
+    with device_outputs=True (torch tensors left in HBM), each with its cost per step split into
+    launch, kernel wait, D2H copies and Python infos; and the single-env gym shim
+    Rocket6DOF.step (one launch + one sync per step) beside the reference's own 569 steps/s."""
+    import numpy as np
+    import torch
+
+    from rl_rocket_amd.envs import Rocket6DOF
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF, MAX_EPISODE_STEPS
+    from rl_rocket_amd.vec_env import RocketVecEnv
+
+    out = {}
+    rng = np.random.default_rng(0)
+    host_pool = [rng.uniform(-1, 1, (n, 3)).astype(np.float32) for _ in range(POOL)]
+
+    def run(venv, acts, k0, count, host=True):
+        n_done = 0
+        for k in range(count):
+            _, _, d, infos = venv.step(acts[(k0 + k) % POOL])
+            if host:  # numpy flags (device flags are left alone: counting them would sync)
+                n_done += int(d.sum())
+        torch.cuda.synchronize(dev)
+        return n_done
+
+    # host outputs: numpy actions in, numpy obs / reward / done + lazy infos out
+    venv = RocketVecEnv(n, model="6DOF", device=dev, max_episode_steps=MAX_EPISODE_STEPS, monitor=True,
+                        **ENV_CONFIG_6DOF)
+    venv.reset()
+    run(venv, host_pool, 0, 10)
+    t0 = time.perf_counter()
+    n_done = run(venv, host_pool, 10, steps)
+    dt = time.perf_counter() - t0
+    venv.timing = {}
+    run(venv, host_pool, 0, steps)
+    split = {k: v / steps * 1e6 for k, v in venv.timing.items()}
+    venv.close()
+    out["vecenv_host"] = {
+        "value": n * steps / dt, "unit": "env-steps/s", "us_per_step": dt / steps * 1e6, "n_envs": n, "steps": steps,
+        "done_per_step": n_done / steps,
+        "split_us_per_step": split,
+        "split_note": "second pass with a synchronize after the launch: launch = action H2D + rr_step call (host), "
+                      "kernel = remaining device time, d2h = obs / reward / done copies to numpy, infos = done list "
+                      "(rr_fetch_done) + terminal_observation / TimeLimit.truncated / Monitor dicts of the done envs",
+        "path": "RocketVecEnv(monitor=True).step(numpy actions) -> numpy obs/reward/done + lazy infos (SB3 VecEnv)"}
+
+    # device outputs: device actions in, device tensors out (obs stay in HBM), Monitor on
+    pool = torch.rand((POOL, n, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(1)) * 2 - 1
+    venv = RocketVecEnv(n, model="6DOF", device=dev, max_episode_steps=MAX_EPISODE_STEPS, monitor=True,
+                        device_outputs=True, **ENV_CONFIG_6DOF)
+    venv.reset()
+    run(venv, pool, 0, 10, host=False)
+    t0 = time.perf_counter()
+    run(venv, pool, 10, steps, host=False)
+    dt = time.perf_counter() - t0
+    venv.timing = {}
+    run(venv, pool, 0, steps, host=False)
+    split = {k: v / steps * 1e6 for k, v in venv.timing.items()}
+    venv.close()
+    out["vecenv_device"] = {
+        "value": n * steps / dt, "unit": "env-steps/s", "us_per_step": dt / steps * 1e6, "n_envs": n, "steps": steps,
+        "split_us_per_step": split,
+        "split_note": "launch = rr_step + the done rows' terminal copy (host time of the async calls); infos = the "
+                      "Monitor build of step t-2's infos (done-flag D2H, which waits for the GPU, + dicts)",
+        "path": "RocketVecEnv(monitor=True, device_outputs=True).step(device actions) -> device tensors + lazy infos"}
+
+    # the single-env gym shim: one env, one launch + one packed D2H per step
+    env = Rocket6DOF(device=dev, **ENV_CONFIG_6DOF)
+    env.reset()
+    a_pool = rng.uniform(-1, 1, (256, 3)).astype(np.float32)
+    for k in range(20):
+        if env.step(a_pool[k])[2]:
+            env.reset()
+    count, t0 = 0, time.perf_counter()
+    while count < 3000 and time.perf_counter() - t0 < 3.0:
+        if env.step(a_pool[count % 256])[2]:
+            env.reset()
+        count += 1
+    dt = time.perf_counter() - t0
+    env.close()
+    out["single_env_gym"] = {
+        "value": count / dt, "unit": "env-steps/s", "us_per_step": dt / count * 1e6, "steps": count,
+        "vs_reference_python_step_survey": count / dt / REFERENCE_PY_STEP["6DOF"],
+        "path": "rl_rocket_amd.envs.Rocket6DOF.step (gym API, N=1 kernel launch + sync per step, reset via gym "
+                "0.21 seeding on the host)"}
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# committed evidence of the same kernel source (rocprofv3 PMC traffic, kernel-trace durations)
+# ---------------------------------------------------------------------------------------------
+def _stored(pattern, model, n, want_hash):
+    import glob
+
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", pattern % n), recursive=True),
+                  key=os.path.getmtime)
+    stale = None
+    for path in reversed(hits):
+        with open(path) as f:
+            d = json.load(f)
+        if not d.get("kernel", "").startswith("step_kernel<%d," % model):
+            continue
+        if d.get("source_hash") == want_hash:
+            return d, os.path.relpath(path, ROOT)
+        stale = stale or os.path.relpath(path, ROOT)
+    return None, ("no file for kernel source %s (latest, other source: %s)" % (want_hash, stale))
 
 
 def stored_traffic(model, n):
     """Per-launch HBM bytes of the same kernel/config from the latest committed rocprofv3 PMC
     passes (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), only if they were measured on
     THIS kernel code (same rl_rocket_amd.build.source_hash); else (None, reason)."""
-    import glob
-
     from rl_rocket_amd.build import source_hash
 
-    want = source_hash()
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "pmc_traffic_n%d.json" % n), recursive=True),
-                  key=os.path.getmtime)
-    stale = None
-    for path in reversed(hits):
-        d = json.load(open(path))
-        if not d.get("kernel", "").startswith("step_kernel<%d," % model):
-            continue
-        if d.get("source_hash") == want:
-            return d["traffic_bytes"], os.path.relpath(path, ROOT)
-        stale = stale or os.path.relpath(path, ROOT)
-    return None, ("no PMC traffic file for kernel source %s (latest, other source: %s)" % (want, stale))
+    d, src = _stored("pmc_traffic_n%d.json", model, n, source_hash())
+    return (d["traffic_bytes"], src) if d else (None, src)
+
+
+def stored_rocprof(model, n, steps):
+    """The step kernel's rocprofv3 kernel-trace mean of the same protocol (tools/rocprof_step.py:
+    a --kernel-trace --stats run of this bench command, committed under profiles/), only if it
+    was measured on THIS kernel code; else (None, reason)."""
+    from rl_rocket_amd.build import source_hash
+
+    d, src = _stored("rocprof_step_k%d_n%%d.json" % steps, model, n, source_hash())
+    return d, src
 
 
 def main():
     args = parse()
-    import numpy as np
+    plan, msg = launch_plan(args.gpus, os.environ)
+    if plan == "error":
+        print(msg, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+
+    import numpy as np  # noqa: F401
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -271,18 +589,20 @@ def main():
     backend = os.environ.get("RR_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    gather_leg = args.mode == "step" and not args.allgather and not args.no_gather_leg and (world > 1 or args.gather_leg)
     dist = None
-    if world == 1 and args.allgather:  # step + gather path on one GPU (a rehearsal of the collective)
+    if world == 1 and (args.allgather or gather_leg):  # step + gather on one GPU (a rehearsal of the collective)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29571")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-    if world > 1 or args.allgather:
+    if world > 1 or args.allgather or gather_leg:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
 
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF, MAX_EPISODE_STEPS, parse_model
@@ -303,112 +623,43 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
     pool = torch.rand((POOL, n, env.action_dim), device=dev, generator=gen) * 2 - 1
-    gather = None
-    if args.allgather and dist is not None:
-        from rl_rocket_amd.dist import ShardGather
-        gather = ShardGather(n, env.state_dim, dev)
-
-    def one(k):
-        if gather is not None:
-            # the step writes obs / reward / done straight into the send rows (rr_step_rows),
-            # then ONE RCCL all_gather over xGMI: the global batch on every rank
-            gather.step(env, pool[k % POOL])
-        else:
-            env.step(pool[k % POOL])
-
-    stream = torch.cuda.current_stream(dev)
     launch = args.launch
     if launch == "auto":
         launch = "loop" if args.steps < AUTO_LOOP_MAX_K and not args.allgather else "graph"
-    use_loop = launch == "loop" and not args.allgather
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if use_loop:
-        # the same call as the timed region (its launch block is written once, here), and the
-        # two timing events created so that the C call can record them
-        ev0.record(stream)
-        ev1.record(stream)
-        env.step_repeat(pool, args.warmup, events=(ev0, ev1))
-    else:
-        for k in range(args.warmup):
-            one(k)
-    torch.cuda.synchronize(dev)
+    gather = None
+    if args.allgather:
+        from rl_rocket_amd.dist import ShardGather
+        gather = ShardGather(n, env.state_dim, dev)
 
-    # ---- timed region: exactly K steps (hipGraph replays) ----
-    # step + all_gather graphs need a capturable collective (RCCL); gloo is a host path
-    use_graph = not args.no_graph and launch == "graph" and not (gather is not None and backend == "gloo")
-    # exactly K steps: K // gs replays of a gs-launch graph (gs balanced so that K = 2000 is
-    # 2 x 1000, not 1024 + 976) plus one graph of the K % gs remainder launches
-    K = args.steps
-    gs = max(1, -(-K // max(1, -(-K // max(1, args.graph_steps)))))
-    rem = K % gs
-
-    def capture(n_launch):
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(stream)
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                for k in range(n_launch):
-                    one(k)
-        stream.wait_stream(s)
-        torch.cuda.synchronize(dev)
-        g.replay()  # warm the graph
-        torch.cuda.synchronize(dev)
-        return g
-
-    if use_graph:
-        graph = capture(gs)
-        graph_rem = capture(rem) if rem else None
-    # Device time of the K launches: HIP events on the launch stream around the replays. It
-    # includes hipGraphLaunch's fixed preamble on the GPU timeline (~6-8 us per replay, so
-    # +0.3-0.4 us per step at the driver's K = 20); event-record nodes inside the graph, which
-    # would exclude it, are refused by torch on ROCm ("External events are disallowed").
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    if use_loop:
-        fn, fargs = env.step_repeat_call(pool, K, (ev0, ev1))
-    t0 = time.perf_counter()
-    if use_loop:
-        # K direct launches from one C call, which records the two HIP events on the launch
-        # stream right before the first and right after the last launch
-        rc = fn(*fargs)
-    else:
-        ev0.record(stream)  # HIP events on the stream the step kernels are launched on
-        if use_graph:
-            for _ in range(K // gs):
-                graph.replay()
-            if graph_rem is not None:
-                graph_rem.replay()
-        else:
-            for k in range(K):
-                one(k)
-        ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if use_loop:
-        from rl_rocket_amd import _lib
-        _lib.check(rc, "rr_step_repeat_timed")
-    # device time per launch over the timed region (kernel + inter-kernel gap inside the
-    # graph: an upper bound on the kernel's own duration, so `achieved` is conservative).
-    # (Events recorded with hipEventReleaseToDevice instead of torch's system-scope release
-    # read the same at K = 20: 4.58 vs 4.56 us per launch, r02o.)
-    kern_ms = ev0.elapsed_time(ev1) / K
-    if dist is not None:  # max over ranks of the timed region
-        t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
+    # ---- the headline timed region ----
+    reg = timed_region(args, env, pool, dev, dist, backend, launch, gather)
+    K, dt, kern_ms = args.steps, reg["dt"], reg["kern_ms"]
     value = n * world * K / dt
     bytes_env = BYTES_PER_STEP[model] + (8 if args.monitor else 0)  # + Monitor return plane read / write
     bytes_launch = bytes_env * n
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    if args.monitor or args.allgather or args.integrator != "rk4":
-        traffic, traffic_src = None, "PMC traffic files cover the headline configuration (RK4, no Monitor, no gather)"
-    else:
+    achieved_wall = bytes_launch / (dt / K) / 1e9
+    headline_cfg = not (args.monitor or args.allgather or args.integrator != "rk4")
+    if headline_cfg:
         traffic, traffic_src = stored_traffic(model, n)
+        rp, rp_src = stored_rocprof(model, n, K)
+    else:
+        traffic, traffic_src = None, "PMC traffic files cover the headline configuration (RK4, no Monitor, no gather)"
+        rp, rp_src = None, "rocprofv3 files cover the headline configuration"
+    if args.integrator == "euler":
+        parity = ("NON-PARITY speed mode (BASELINE configs[1] 'Euler integrator'): explicit Euler misses the "
+                  "reference's RK45 by 30-130x the 1e-5 bar (SURVEY.md §7; tests/test_gpu_envs.py::"
+                  "test_euler_mode_is_declared_non_parity)")
+    elif args.integrator == "dopri5":
+        parity = ("exact mode: fp64 scipy RK45 + brentq restated, <= 4.4e-9 floored-relative vs the reference's "
+                  "rows (tests/test_gpu_exact.py)")
+    else:
+        parity = ("fp32 RK4 + Hermite ground event, <= 1e-5 floored-relative vs the reference's rows and the "
+                  "oracle (tests/test_gpu_parity.py)")
+    rocprof = None
+    if rp is not None:
+        rocprof = {"mean_us": rp["mean_ns"] / 1e3, "frac": bytes_launch / (rp["mean_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS,
+                   "calls": rp["calls"], "events_us_same_run": rp.get("events_kernel_us"), "source": rp_src}
     result = {
         "metric": "env-steps/sec (%s, N=%d per GPU)" % ("6DOF" if model == 6 else "3DOF", n),
         "value": value,
@@ -420,34 +671,60 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp64" if args.integrator == "dopri5" else "fp32",
+        "parity": parity,
         "data": "synthetic: ICs ~ U(init_space of configuration_file.env_config), actions ~ U(-1,1) seeded pool of %d "
                 "batches resident in HBM" % POOL,
         "config": {"workload": "Rocket%s N=%d per GPU, %s fused step+reward+TimeLimit(800)+auto-reset, %s"
                                % ("6DOF" if model == 6 else "3DOF", n, args.integrator.upper(),
-                                  "step rows + RCCL all_gather of obs/reward/done each step" if args.allgather else
+                                  "step rows + all_gather of obs/reward/done each step" if args.allgather else
                                   "no data-path collective") + (", Monitor returns" if args.monitor else ""),
                    "envs_per_gpu": n, "global_envs": n * world, "integrator": args.integrator,
-                   "graph_steps": gs if use_graph else 0, "launch": "graph" if use_graph else
-                   ("direct: rr_step_repeat_timed" if use_loop else "rr_step per step"),
-                   "parallelism": "env-sharded x%d" % world},
+                   "graph_steps": reg["gs"] if reg["use_graph"] else 0, "launch": "graph" if reg["use_graph"] else
+                   ("direct: tools/libbench_timed.so (K rr_step calls)" if reg["use_loop"] else "rr_step per step"),
+                   "parallelism": "env-sharded x%d" % world,
+                   "world_size": dist.get_world_size() if dist is not None else 1,
+                   "backend": dist.get_backend() if dist is not None else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "B/launch",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "frac_wall": achieved_wall / HBM_PEAK_GBS,
+                     "frac_rocprof": rocprof["frac"] if rocprof else None,
+                     "rocprof": rocprof if rocprof else {"source": rp_src},
+                     "traffic": traffic, "traffic_unit": "B/launch",
                      "traffic_source": traffic_src,
                      "kernel": "step_kernel<%d,%s>" % (model, args.integrator.upper()),
                      "kernel_us": kern_ms * 1e3,
-                     "timing": "HIP events on the launch stream around the K launches of the timed region" +
-                               (" (recorded by rr_step_repeat_timed itself; the first 2 launches are queued "
-                                "behind a host-released gate kernel so the host's submission stays ahead)"
-                                if use_loop else " (around the hipGraph replays)") +
-                               (" (each step = rr_step_rows + the RCCL all_gather, so kernel_us includes the "
-                                "collective)" if gather is not None else ""),
+                     "timing": "frac: HIP events on the launch stream around the K launches of the timed region" +
+                               (" (recorded by tools/libbench_timed.so; the first 2 launches are queued behind a "
+                                "host-released gate kernel so the host's submission stays ahead)"
+                                if reg["use_loop"] else " (around the hipGraph replays)") +
+                               (" (each step = rr_step_rows + the all_gather, so kernel_us includes the "
+                                "collective)" if gather is not None else "") +
+                               "; frac_wall: the same bytes over the wall-clock ms_per_step; frac_rocprof: over the "
+                               "rocprofv3 kernel-trace mean of this command on this kernel source (committed "
+                               "under profiles/)",
                      "bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": bytes_env},
     }
+
+    # ---- the step + all_gather leg (reported separately from the step alone) ----
+    if gather_leg:
+        from rl_rocket_amd.dist import ShardGather
+        g = ShardGather(n, env.state_dim, dev)
+        greg = timed_region(args, env, pool, dev, dist, backend, "graph" if launch == "loop" else launch, g)
+        result["allgather"] = {
+            "value": n * world * K / greg["dt"], "unit": "env-steps/s", "ms_per_step": greg["dt"] / K * 1e3,
+            "device_us_per_step": greg["kern_ms"] * 1e3,
+            "world_size": dist.get_world_size(), "backend": dist.get_backend(),
+            "bytes_per_rank_per_step": g.n_pad * (env.state_dim + 2) * 4,
+            "launch": "graph" if greg["use_graph"] else "eager (gloo stages through the host)",
+            "what": "rr_step_rows into the send rows + ONE all_gather_into_tensor of [N][state_dim+2] fp32 rows "
+                    "(obs, reward, done) per step, the global batch on every rank (ShardGather.step)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baselines(model, args.cpu_seconds, host_cores())
     env.close()
+    if rank == 0 and world == 1 and model == 6 and not args.no_sb3_legs and args.integrator == "rk4":
+        result["sb3_legs"] = sb3_legs(dev, n, args.sb3_steps)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 6
+#define RR_ABI_VERSION 7
 
 /* error codes */
 #define RR_OK 0
@@ -134,7 +134,10 @@ int rr_action_dim(const rr_env* e);
  * (the seed's four key words — splitmix64 of `seed` on the host — , gid, cw): deterministic,
  * independent of how envs are sharded over GPUs, and free of per-env RNG state in HBM. The
  * episode field has 32 - rr_counter_bits() bits (22 under the reference's TimeLimit 800), so
- * one env's keys do not repeat for 2^22 episodes. Host-only call. */
+ * one env's keys do not repeat for 2^22 episodes. Host-only call: it synchronises the device
+ * (no kernel still in flight reads the old key) and the new key applies to every launch that
+ * runs after it, including replays of hipGraphs captured before it, at every N. `stream` is
+ * unused (kept for ABI stability). */
 int rr_seed(rr_env* e, uint64_t seed, void* stream);
 /* Sample a fresh initial condition for every env where mask[i] != 0 (all when mask is
  * NULL), write the normalised obs [N][state_dim] (obs may be NULL). */
@@ -168,22 +171,15 @@ int rr_step_rows(rr_env* e, const float* action, float* rows, uint8_t* truncated
  * last step. */
 int rr_step_repeat(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs, float* reward,
                    uint8_t* done, uint8_t* truncated, float* terms, void* stream);
-/* rr_step_repeat with a pair of hipEvent_t (as void*; both or neither) recorded on `stream`
- * right before the first and right after the last of the n_steps launches, for an event-timed
- * region that holds exactly those launches (bench.py --launch loop). The stream is held behind
- * a one-wave gate kernel (time-bounded, 1 s) that the call releases once the first 2 launches
- * are submitted: the host (~3 us per direct launch) then stays ahead of the GPU (~4.4 us per
- * step at N = 65536), so the region measures back-to-back launches rather than the host's
- * submission pace. Not capturable. (ABI v6) */
-int rr_step_repeat_timed(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs,
-                         float* reward, uint8_t* done, uint8_t* truncated, float* terms, void* stream,
-                         void* ev_start, void* ev_end);
-
 /* Overwrite / read the per-env state (parity injection, checkpoint / restore).
  * state_soa [state_dim][N] fp32; v0 [N] or NULL (kept on set / skipped on get);
  * elapsed [N] or NULL is the per-env counter word: TimeLimit steps in bits 0..E-1, episodes
  * started in bits E..31 (keys the reset stream), E = rr_counter_bits(e); a plain step count
- * is a valid word (episode 0). On set, NULL clears the steps and keeps the episode field.
+ * below 2^E is a valid word (episode 0; larger counts would spill into the episode field: the
+ * Python layer rejects them). On set, NULL clears the steps and keeps the episode field. The
+ * elapsed field saturates at 2^E - 1 (>= max_episode_steps): an env stepped on past its
+ * TimeLimit without a reset keeps reporting done / truncated; its Monitor length and, under
+ * RR_INT_DOPRI5, its clock t = steps * dt stop there.
  * rr_set_state* zero the Monitor running return (an injected state starts a new segment);
  * rr_get_aux / rr_set_aux round-trip the raw counter words and the running return for a
  * checkpoint. */
@@ -211,8 +207,10 @@ int rr_get_buffers(rr_env* e, rr_buffers* out);
 int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs, float* term_return,
                       int32_t* term_len, void* stream);
 
-/* Device-to-device copy of the full per-env terminal buffers of the last step
- * (rows valid where done[i]); any destination may be NULL. Asynchronous. */
+/* Device-to-device copy of the terminal rows of the envs done at the last step (their final
+ * obs row [state_dim], episode return, episode length) into the same rows of the caller's
+ * [N][state_dim] / [N] / [N] buffers; rows of envs not done are left untouched. Any destination
+ * may be NULL. One kernel that reads the last step's done masks. Asynchronous. */
 int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* term_len, void* stream);
 
 /* ---- On-device PPO rollouts (BASELINE configs[4]) ----

@@ -8,12 +8,13 @@ loader reuses the already-loaded copy).
 """
 import ctypes
 import os
+import warnings
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
@@ -94,7 +95,6 @@ SIGNATURES = {
     "rr_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "rr_step_rows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "rr_step_repeat": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, _P]),
-    "rr_step_repeat_timed": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rr_set_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_get_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_set_state64": (ctypes.c_int, [_P, _P, _P, _P, _P]),
@@ -139,16 +139,33 @@ def load(require_torch=True):
             "librocket_hip.so is not built (expected at %s). Build it with "
             "`python -m rl_rocket_amd.build` (hipcc, gfx950). There is no CPU fallback." % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
+    override = bool(os.environ.get("RR_LIB_PATH"))
+    missing = []
     for name, (res, args) in SIGNATURES.items():
-        if os.environ.get("RR_LIB_PATH") and not hasattr(lib, name):
-            continue  # an older diagnostic build (tools/ab_kernel.py) may lack newer entry points
+        if override and not hasattr(lib, name):
+            missing.append(name)  # an older diagnostic build (tools/ab_kernel.py) may lack newer entry points
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rr_abi_version() != ABI_VERSION and not os.environ.get("RR_LIB_PATH"):  # diagnostic builds may be older
-        raise RocketHipError("librocket_hip.so ABI %d != expected %d" % (lib.rr_abi_version(), ABI_VERSION))
+    abi = lib.rr_abi_version()
+    if abi != ABI_VERSION:
+        if not override:
+            raise RocketHipError("librocket_hip.so ABI %d != expected %d" % (abi, ABI_VERSION))
+        # diagnostic builds may be older: say so now rather than as a wrong counter decoding later
+        warnings.warn("RR_LIB_PATH=%s has ABI %d, this package expects %d%s" % (
+            LIB_PATH, abi, ABI_VERSION, (" (missing: %s)" % ", ".join(missing)) if missing else ""),
+            RuntimeWarning, stacklevel=2)
+    for name in missing:  # a call of a missing entry point raises a clear error at the call site
+        setattr(lib, name, _missing(name))
     _LIB = lib
     return lib
+
+
+def _missing(name):
+    def call(*a, **k):
+        raise RocketHipError("%s is not exported by the RR_LIB_PATH library %s (ABI mismatch)" % (name, LIB_PATH))
+    return call
 
 
 def check(rc, what="rocket_hip"):

@@ -122,49 +122,26 @@ class RocketBatch:
                                          self._stream()), "rr_step_rows")
         return rows
 
-    def step_repeat_call(self, actions, n_steps, events):
-        """(function, arguments) of the rr_step_repeat_timed call that step_repeat(actions, n_steps,
-        events) makes, prepared once (bench.py times the bare C call)."""
-        t = self.torch
-        if not isinstance(actions, t.Tensor) or actions.device != self.device or actions.dtype != t.float32:
-            raise TypeError("actions must be a float32 tensor on %s" % self.device)
-        shape = (self.action_dim, self.num_envs) if self.action_soa else (self.num_envs, self.action_dim)
-        if not actions.is_contiguous() or tuple(actions.shape[1:]) != shape:
-            raise ValueError("actions must be a contiguous [B]%s tensor" % (list(shape),))
-        ev = [ctypes.c_void_p(e.cuda_event) for e in events]
-        if not all(e.value for e in ev):
-            raise ValueError("step_repeat: the events must exist (record them once before timing)")
-        self._last_action = actions
-        return self.lib.rr_step_repeat_timed, (self._h, _ptr(actions), actions.shape[0], int(n_steps), _ptr(self.obs),
-                                               _ptr(self.reward), _ptr(self.done), _ptr(self.truncated),
-                                               _ptr(self.terms), self._stream(), ev[0], ev[1])
-
-    def step_repeat(self, actions, n_steps, events=None):
+    def step_repeat(self, actions, n_steps):
         """`n_steps` consecutive steps, step t taking action batch t % len(actions) of the device
         tensor `actions` [B][N][action_dim] (rr_step_repeat: one host call, direct dispatch).
-        `events` = (start, end) torch.cuda.Event pair recorded right before the first and right
-        after the last launch (rr_step_repeat_timed). Returns the output tensors of the last step."""
+        Returns the output tensors of the last step."""
         t = self.torch
         if not isinstance(actions, t.Tensor) or actions.device != self.device or actions.dtype != t.float32:
             raise TypeError("actions must be a float32 tensor on %s" % self.device)
         shape = (self.action_dim, self.num_envs) if self.action_soa else (self.num_envs, self.action_dim)
         actions = actions.reshape((-1,) + shape).contiguous()
         self._last_action = actions
-        args = (self._h, _ptr(actions), actions.shape[0], int(n_steps), _ptr(self.obs), _ptr(self.reward),
-                _ptr(self.done), _ptr(self.truncated), _ptr(self.terms), self._stream())
-        if events is None:
-            _lib.check(self.lib.rr_step_repeat(*args), "rr_step_repeat")
-        else:
-            ev = [ctypes.c_void_p(e.cuda_event) for e in events]
-            if not all(e.value for e in ev):
-                raise ValueError("step_repeat: the events must exist (record them once before timing)")
-            _lib.check(self.lib.rr_step_repeat_timed(*args, ev[0], ev[1]), "rr_step_repeat_timed")
+        _lib.check(self.lib.rr_step_repeat(self._h, _ptr(actions), actions.shape[0], int(n_steps), _ptr(self.obs),
+                                           _ptr(self.reward), _ptr(self.done), _ptr(self.truncated), _ptr(self.terms),
+                                           self._stream()), "rr_step_repeat")
         return self.obs, self.reward, self.done, self.truncated
 
     def set_state(self, state_soa, v0=None, elapsed=None):
         """Inject fp32 state planes [state_dim][N]; v0 [N] (kept when None); `elapsed` = counter
-        words [N] (a plain step count is episode 0; None clears the steps and keeps the episode
-        field). Zeroes the Monitor running return (restore() keeps it)."""
+        words [N] (a plain step count below 2^counter_bits is episode 0 — build words for larger
+        values with make_counter(), which range-checks them; None clears the steps and keeps the
+        episode field). Zeroes the Monitor running return (restore() keeps it)."""
         t = self.torch
         st = t.as_tensor(state_soa, device=self.device, dtype=t.float32).reshape(self.state_dim, self.num_envs)
         st = st.contiguous()
@@ -195,9 +172,17 @@ class RocketBatch:
         return c & ((1 << e) - 1), c >> e
 
     def make_counter(self, elapsed, episode=0):
-        """Counter words from elapsed steps and episode numbers (int32 view of the u32 word)."""
+        """Counter words from elapsed steps and episode numbers (int32 view of the u32 word).
+        Raises if an elapsed count does not fit the E-bit field (it would spill into the episode
+        field, which keys the reset stream) or an episode number the 32 - E bits above it."""
         e = self.counter_bits
-        w = (np.asarray(episode, np.int64) << e) | np.asarray(elapsed, np.int64)
+        el = np.asarray(elapsed, np.int64)
+        ep = np.asarray(episode, np.int64)
+        if (el < 0).any() or (el >= (1 << e)).any():
+            raise ValueError("elapsed steps must be in [0, %d) (the counter word's %d-bit field)" % (1 << e, e))
+        if (ep < 0).any() or (ep >= (1 << (32 - e))).any():
+            raise ValueError("episode numbers must be in [0, 2^%d)" % (32 - e))
+        w = (ep << e) | el
         return (w & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
 
     def checkpoint(self):
@@ -252,13 +237,14 @@ class RocketBatch:
         return idx[:m], tobs[:m], ret[:m], ln[:m]
 
     def copy_terminal(self, out=None):
-        """Device copies of the per-env terminal buffers (rows valid where done). `out` =
-        preallocated (obs [N,ns] f32, return [N] f32, len [N] i32), any may be None."""
+        """Device copies of the terminal rows of the envs done at the last step (rr_copy_terminal:
+        only those rows are written). `out` = preallocated (obs [N,ns] f32, return [N] f32, len
+        [N] i32), any may be None; by default fresh zero-filled tensors."""
         t = self.torch
         if out is None:
-            out = (t.empty((self.num_envs, self.state_dim), dtype=t.float32, device=self.device),
-                   t.empty((self.num_envs,), dtype=t.float32, device=self.device),
-                   t.empty((self.num_envs,), dtype=t.int32, device=self.device))
+            out = (t.zeros((self.num_envs, self.state_dim), dtype=t.float32, device=self.device),
+                   t.zeros((self.num_envs,), dtype=t.float32, device=self.device),
+                   t.zeros((self.num_envs,), dtype=t.int32, device=self.device))
         tobs, ret, ln = out
         _lib.check(self.lib.rr_copy_terminal(self._h, _ptr(tobs), _ptr(ret), _ptr(ln), self._stream()),
                    "rr_copy_terminal")

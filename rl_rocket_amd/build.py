@@ -13,6 +13,9 @@ SRC = os.path.join(HERE, "csrc", "rocket_hip.hip")
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc", "rocket_rollout.inc")]
 HEADER = os.path.join(ROOT, "include", "rocket_hip.h")
 OUT = os.path.join(HERE, "librocket_hip.so")
+# benchmark-only helper (not part of the product ABI): bench.py's event-timed direct-launch region
+BENCH_SRC = os.path.join(ROOT, "tools", "bench_timed.hip")
+BENCH_OUT = os.path.join(ROOT, "tools", "libbench_timed.so")
 ARCH = os.environ.get("RR_OFFLOAD_ARCH", "gfx950")
 
 
@@ -63,6 +66,7 @@ def up_to_date():
 
 
 def build(force=False, resource_usage=False, verbose=True):
+    build_bench_helper(force=force, verbose=verbose)
     if not force and up_to_date():
         return OUT
     cmd = command(resource_usage)
@@ -70,6 +74,18 @@ def build(force=False, resource_usage=False, verbose=True):
         print("[rl_rocket_amd.build]", " ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=ROOT)
     return OUT
+
+
+def build_bench_helper(force=False, verbose=True):
+    """tools/libbench_timed.so: the gate kernel + event-timed launch loop bench.py uses below
+    K = 32 timed steps (it drives the library through its public rr_step)."""
+    if not force and os.path.exists(BENCH_OUT) and os.path.getmtime(BENCH_OUT) >= os.path.getmtime(BENCH_SRC):
+        return BENCH_OUT
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-o", BENCH_OUT, BENCH_SRC]
+    if verbose:
+        print("[rl_rocket_amd.build]", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd, cwd=ROOT)
+    return BENCH_OUT
 
 
 if __name__ == "__main__":

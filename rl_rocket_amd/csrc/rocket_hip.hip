@@ -205,14 +205,16 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
 struct Bufs {
     float* state;
     float* v0;
-    uint32_t* counter;        // [N] elapsed | episode << 16
+    uint32_t* counter;        // [N] counter word: elapsed in bits 0..E-1, episode above (E = KParams.ep_shift)
     float* ep_ret;
     uint64_t* done_bits;      // [ceil(N/64)] wave ballot of done lanes, one word per wave
     float* term_obs;
     float* term_ret;
     int32_t* term_len;
     int64_t n;
-    const KParams* kp;        // device copy of the kernel's KParams (helper waves read it: see step_kernel)
+    const KParams* kp;        // device copy of the kernel's KParams: the helper waves read it (see step_kernel),
+                              // and every kernel reads the reset-stream key seed_w from it, so rr_seed applies
+                              // to every later launch, graph replays included
 };
 
 struct StepIO {
@@ -981,10 +983,12 @@ struct CounterLayout {
         pin_s(max_steps);
     }
     // gym TimeLimit (main_6DOF.py:21): elapsed += 1; at the limit done = True and
-    // info["TimeLimit.truncated"] = not done. Returns the new elapsed count.
+    // info["TimeLimit.truncated"] = not done. Returns the new elapsed count, saturated at el_mask
+    // (>= max_steps): an env stepped on past its TimeLimit without a reset keeps reporting
+    // done / truncated instead of wrapping into the episode field.
     __device__ __forceinline__ int32_t time_limit(uint32_t cw, bool& done, bool& trunc) const
     {
-        const int32_t el = (int32_t)(cw & el_mask) + 1;
+        const int32_t el = min((int32_t)(cw & el_mask) + 1, (int32_t)el_mask);
         trunc = false;
         if (max_steps > 0 && el >= max_steps) {
             trunc = !done;
@@ -1142,7 +1146,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     // last. Used by done lanes only. (HELP: drawn by the helper wave instead.)
     float ic_s[NS], ic_v0 = 0.0f;
     if (!HELP && (mode & RR_FLAG_AUTO_RESET)) {
-        ResetStream key = reset_stream(P.seed_w, P.id_off + i, cw);
+        ResetStream key = reset_stream(B.kp->seed_w, P.id_off + i, cw);
         sample_ic<MODEL>(P, key, ic_s, ic_v0);
     }
 
@@ -1219,7 +1223,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const KParams P, const Bu
     float s[NS], v0;
     if (mask == nullptr || mask[i]) {
         const uint32_t ep = (B.counter[i] >> P.ep_shift) + 1u;
-        ResetStream key = reset_stream(P.seed_w, P.id_off + i, B.counter[i]);
+        ResetStream key = reset_stream(B.kp->seed_w, P.id_off + i, B.counter[i]);
         sample_ic<MODEL>(P, key, s, v0);
 #pragma unroll
         for (int j = 0; j < NS; ++j) B.state[(int64_t)j * n + i] = s[j];
@@ -1259,6 +1263,21 @@ __global__ __launch_bounds__(kBlock) void gather_done_kernel(const int32_t* idx,
     for (int j = 0; j < ns; ++j) g_obs[k * ns + j] = term_obs[i * ns + j];
     g_ret[k] = term_ret[i];
     g_len[k] = term_len[i];
+}
+
+// rr_copy_terminal: the terminal rows of the envs done at the last step (done_bits) into
+// caller buffers (any may be null); rows of other envs are left untouched
+__global__ __launch_bounds__(kBlock) void copy_done_rows_kernel(const uint64_t* done_bits, int64_t n, int ns,
+                                                                const float* term_obs, const float* term_ret,
+                                                                const int32_t* term_len, float* d_obs, float* d_ret,
+                                                                int32_t* d_len)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || !((done_bits[i / kWave] >> (i % kWave)) & 1ull)) return;
+    if (d_obs)
+        for (int j = 0; j < ns; ++j) d_obs[i * ns + j] = term_obs[i * ns + j];
+    if (d_ret) d_ret[i] = term_ret[i];
+    if (d_len) d_len[i] = term_len[i];
 }
 
 // On-device PPO rollout kernels (fused MlpPolicy forward on fp32 MFMA, bootstrap, GAE)
@@ -1440,8 +1459,6 @@ struct rr_env {
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
     KParams* d_kp;      // device copy of kp (Bufs.kp)
-    uint32_t* gate;     // host-pinned word releasing gate_kernel (rr_step_repeat_timed)
-    uint32_t gate_gen;
     int32_t* g_idx;     // rr_fetch_done scratch
     float* g_obs;
     float* g_ret;
@@ -1560,9 +1577,6 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->kp.id_off = env_id_offset;
     {
         hipError_t err = hipMalloc((void**)&e->d_kp, sizeof(KParams));
-        if (err == hipSuccess) err = hipHostMalloc((void**)&e->gate, 64, hipHostMallocCoherent);
-        if (err == hipSuccess) __atomic_store_n(e->gate, 0u, __ATOMIC_SEQ_CST);
-        else e->gate = nullptr;
         if (err != hipSuccess) {
             rr_destroy(e);
             return hip_fail(err, "rr_create: hipMalloc (params)");
@@ -1589,7 +1603,6 @@ int rr_destroy(rr_env* e)
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
-    if (e->gate) (void)hipHostFree(e->gate);
     delete e;
     return RR_OK;
 }
@@ -1600,12 +1613,18 @@ int rr_action_dim(const rr_env* e) { return e ? e->na : -1; }
 
 int rr_seed(rr_env* e, uint64_t seed, void* stream)
 {
-    // the reset stream is counter-based: the seed is a kernel argument, and helper waves read it
-    // from the device copy, updated in stream order (it applies to every later launch)
+    // The reset stream is counter-based and every kernel reads its key from the device copy of
+    // the parameters (Bufs.kp), so the new key applies to every launch that runs after this call
+    // — graph replays of launches captured before it included — whatever the batch size. The
+    // device is synchronised first: no kernel still running on any stream reads the copy while
+    // it is rewritten.
+    (void)stream;
     if (!e) return fail(RR_EINVAL, "rr_seed: null handle");
+    DeviceGuard g(e->device);
+    hipError_t err = hipDeviceSynchronize();
+    if (err != hipSuccess) return hip_fail(err, "rr_seed: device sync");
     seed_words(seed, e->kp.seed_w);
-    hipError_t err = hipMemcpyAsync(e->d_kp, &e->kp, sizeof(KParams), hipMemcpyHostToDevice, (hipStream_t)stream);
-    if (err == hipSuccess) err = hipStreamSynchronize((hipStream_t)stream);
+    err = hipMemcpy(e->d_kp, &e->kp, sizeof(KParams), hipMemcpyHostToDevice);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_seed: params upload");
 }
 
@@ -1626,20 +1645,6 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
 }  // extern "C"
 
 namespace {
-constexpr int64_t kGateQueued = 2;                  // launches queued behind the gate before its release
-constexpr uint64_t kGateMaxTicks = 100000000ull;    // 1 s of the 100 MHz realtime clock
-
-// One wave holds the stream until the host-written word reaches `gen` (rr_step_repeat_timed),
-// or `ticks` of the 100 MHz realtime clock pass: every path exits.
-__global__ __launch_bounds__(64) void gate_kernel(const uint32_t* word, uint32_t gen, uint64_t ticks)
-{
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) break;
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
 // one step launch (rr_step / rr_step_repeat; arguments checked by the caller)
 template <bool ROWS>
 int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
@@ -1732,55 +1737,13 @@ int rr_step_rows(rr_env* e, const float* action, float* rows, uint8_t* truncated
 int rr_step_repeat(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs, float* reward,
                    uint8_t* done, uint8_t* truncated, float* terms, void* stream)
 {
-    return rr_step_repeat_timed(e, actions, n_batches, n_steps, obs, reward, done, truncated, terms, stream, nullptr,
-                                nullptr);
-}
-
-int rr_step_repeat_timed(rr_env* e, const float* actions, int64_t n_batches, int64_t n_steps, float* obs,
-                         float* reward, uint8_t* done, uint8_t* truncated, float* terms, void* stream,
-                         void* ev_start, void* ev_end)
-{
     if (!e) return fail(RR_EINVAL, "rr_step_repeat: null handle");
     if (!actions || !obs || !reward || !done) return fail(RR_EINVAL, "rr_step_repeat: actions/obs/reward/done required");
     if (n_batches <= 0 || n_steps < 0) return fail(RR_EINVAL, "rr_step_repeat: n_batches must be >= 1, n_steps >= 0");
-    if (!ev_start != !ev_end) return fail(RR_EINVAL, "rr_step_repeat_timed: give both events or neither");
-    hipStream_t s = (hipStream_t)stream;
-    hipError_t err = hipSuccess;
-    // Timed form: the stream is held by gate_kernel until the first kGateQueued launches of the
-    // region have been submitted (2: the wall clock waits for as few as possible). A direct launch costs ~3 us of host time against ~4.4 us of
-    // GPU time per step at N = 65536, so from there on the host stays ahead and the events
-    // bracket back-to-back launches on the GPU timeline (without the gate the GPU idles while
-    // the first launch is submitted, and a stall of the submitting thread early in a short
-    // region lands inside it); released early so the wall clock does not wait for all K.
-    const bool gate = ev_start != nullptr;
-    if (ev_start) {
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        err = hipStreamIsCapturing(s, &cap);
-        if (err != hipSuccess) return hip_fail(err, "rr_step_repeat_timed: stream query");
-        if (cap != hipStreamCaptureStatusNone) return fail(RR_EINVAL, "rr_step_repeat_timed: not capturable");
-    }
-    if (gate) {
-        ++e->gate_gen;
-        hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)e->gate, e->gate_gen,
-                           (uint64_t)kGateMaxTicks);
-        err = hipGetLastError();
-        if (err != hipSuccess) return hip_fail(err, "rr_step_repeat_timed: gate launch");
-    }
-    int rc = RR_OK;
-    if (ev_start && (err = hipEventRecord((hipEvent_t)ev_start, s)) != hipSuccess)
-        rc = hip_fail(err, "rr_step_repeat_timed: start event");
     const int64_t batch = e->n * e->na;
-    bool held = gate;
-    for (int64_t t = 0; t < n_steps && rc == RR_OK; ++t) {
+    int rc = RR_OK;
+    for (int64_t t = 0; t < n_steps && rc == RR_OK; ++t)
         rc = launch_step<false>(e, actions + (t % n_batches) * batch, obs, reward, done, truncated, terms, stream);
-        if (held && t + 1 >= kGateQueued) {
-            __atomic_store_n(e->gate, e->gate_gen, __ATOMIC_SEQ_CST);
-            held = false;
-        }
-    }
-    if (rc == RR_OK && ev_end && (err = hipEventRecord((hipEvent_t)ev_end, s)) != hipSuccess)
-        rc = hip_fail(err, "rr_step_repeat_timed: end event");
-    if (held) __atomic_store_n(e->gate, e->gate_gen, __ATOMIC_SEQ_CST);  // released on every path
     return rc;
 }
 
@@ -1965,14 +1928,14 @@ int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs
 int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* term_len, void* stream)
 {
     if (!e) return fail(RR_EINVAL, "rr_copy_terminal: null handle");
-    hipStream_t s = (hipStream_t)stream;
-    hipError_t err = hipSuccess;
-    if (term_obs)
-        err = hipMemcpyAsync(term_obs, e->term_obs, sizeof(float) * e->ns * e->n, hipMemcpyDeviceToDevice, s);
-    if (err == hipSuccess && term_return)
-        err = hipMemcpyAsync(term_return, e->term_ret, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
-    if (err == hipSuccess && term_len)
-        err = hipMemcpyAsync(term_len, e->term_len, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    if (!term_obs && !term_return && !term_len) return RR_OK;
+    if (e->steps == 0) return RR_OK;  // no step yet: no done rows
+    // only the rows of the envs done at the last step (its done_bits): ~1 % of the rows in steady
+    // state, so one pass reads N/8 bytes of masks instead of copying the whole [N][state_dim] buffer
+    hipLaunchKernelGGL(copy_done_rows_kernel, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       e->done_bits, e->n, e->ns, e->term_obs, e->term_ret, e->term_len, term_obs, term_return,
+                       term_len);
+    hipError_t err = hipGetLastError();
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_copy_terminal");
 }
 
@@ -2117,11 +2080,8 @@ int launch_rollout(rr_env* e, const char* who, bool multi, const float* params, 
     const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
     const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
     const dim3 grid((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock));
-    // rr_rollout_collect: 64 envs per wave; RR_ROLLOUT_NT=1 selects 32 envs per wave (two waves
-    // per SIMD; measured 2-16 % slower at N = 65536: the env step's VALU work doubles). Read per
-    // call, so tests cover both shapes in one process.
-    const char* ntv = std::getenv("RR_ROLLOUT_NT");
-    const int ntw = (multi && ntv && std::atoi(ntv) == 1) ? 1 : 2;
+    // 64 envs per wave (two 32-env MFMA column tiles). 32 envs per wave (rol::Shape<1>, two waves
+    // per SIMD) measured 2-16 % slower at N = 65536 in round 2: the env step's VALU work doubles.
     hipStream_t s = (hipStream_t)stream;
     const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
 #define RR_LAUNCH(M, I, PR)                                                                                        \
@@ -2129,11 +2089,8 @@ int launch_rollout(rr_env* e, const char* who, bool multi, const float* params, 
         if (!multi)                                                                                                \
             hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, false, 2>), grid, dim3(rol::Shape<2>::kThreads), 0, \
                                s, e->state, nn, mode, e->kp, b, io);                                               \
-        else if (ntw == 2)                                                                                         \
-            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true, 2>), grid, dim3(rol::Shape<2>::kThreads), 0,  \
-                               s, e->state, nn, mode, e->kp, b, io);                                               \
         else                                                                                                       \
-            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true, 1>), grid, dim3(rol::Shape<1>::kThreads), 0,  \
+            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true, 2>), grid, dim3(rol::Shape<2>::kThreads), 0,  \
                                s, e->state, nn, mode, e->kp, b, io);                                               \
     } while (0)
 #define RR_LAUNCH_P(M, I)                                           \

@@ -207,6 +207,51 @@ class Rocket6DOF(_RocketBase):
 
         return pd.DataFrame(self.vtarg_history, columns=["v_x", "v_y", "v_z"])
 
+    # -- episode figures read by EpisodeAnalyzer (rocket_env.py:861-950; plotly imported lazily) ----------------
+    @staticmethod
+    def _plotly():
+        try:
+            import plotly.express as px
+        except ImportError as e:  # pragma: no cover - plotly ships with this image
+            raise ImportError("the episode figures (get_trajectory_plotly & co.) need plotly") from e
+        return px
+
+    def _trajectory_plot_from_df(self, df):
+        """3D trajectory, landing pad disc (radius target_r at x = 0) and velocity cones."""
+        px = self._plotly()
+        fig = px.line_3d(df[["x", "y", "z"]], x="x", y="y", z="z")
+        g = np.linspace(-self.target_r, self.target_r, 100)
+        zv, yv = np.meshgrid(g, g)
+        pad = 1.0 * (zv ** 2 + yv ** 2 < self.target_r ** 2)
+        fig.add_surface(x=pad, y=yv, z=zv, surfacecolor=pad, showscale=False)
+        fig.add_cone(x=df["x"], y=df["y"], z=df["z"], u=df["vx"], v=df["vy"], w=df["vz"], sizeref=3)
+        fig.update_layout(scene_aspectmode="data")
+        return fig
+
+    def _vtarg_plot_figure(self, df):
+        """3D trajectory with the target-velocity field v_targ along it and the landing target."""
+        px = self._plotly()
+        vt = self.vtarg_to_dataframe()
+        k = min(len(df), len(vt))  # vtarg_history has one row per step, the states one more (the IC)
+        fig = px.line_3d(df[["x", "y", "z"]], x="x", y="y", z="z")
+        fig.update_layout(scene_camera=dict(up=dict(x=1, y=0, z=0), center=dict(x=0, y=0, z=0),
+                                            eye=dict(x=0.625, y=1.25, z=0.0)))
+        x_f, y_f, z_f = self.landing_target
+        fig.add_scatter3d(x=[x_f], y=[y_f], z=[z_f])
+        fig.add_cone(x=df["x"][:k], y=df["y"][:k], z=df["z"][:k], u=vt["v_x"][:k], v=vt["v_y"][:k], w=vt["v_z"][:k],
+                     sizeref=3)
+        fig.update_layout(scene_aspectmode="data")
+        return fig
+
+    def get_trajectory_plotly(self):
+        return self._trajectory_plot_from_df(self.states_to_dataframe())
+
+    def get_attitude_trajectory(self):
+        return self._plotly().line(self.states_to_dataframe()[["q0", "q1", "q2", "q3"]])
+
+    def get_vtarg_trajectory(self):
+        return self._vtarg_plot_figure(self.states_to_dataframe())
+
     @property
     def rotation_obj(self):
         from scipy.spatial.transform import Rotation

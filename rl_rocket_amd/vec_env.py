@@ -18,9 +18,10 @@ otherwise numpy arrays as SB3 expects. Device outputs are double-buffered: the t
 returned by step t (and reset) stay unchanged through step t + 1 and are overwritten by
 step t + 2 — what SB3's collect_rollouts needs (it stores ``_last_obs`` from step t after
 stepping t + 1). Their ``infos`` are built lazily from a per-step device snapshot (done /
-truncated flags and terminal rows of THAT step), so reading them late still describes their
-own step; infos nobody reads are built before their snapshot is reused, so every finished
-episode reaches the Monitor statistics, in step order.
+truncated flags and the terminal rows of THAT step's done envs, copied device to device), so
+reading them late still describes their own step. With ``monitor=True`` infos nobody reads are
+built before their snapshot is reused, so every finished episode reaches the Monitor statistics
+in step order; without it an unread snapshot is dropped unbuilt and nothing leaves HBM.
 """
 import time
 from collections.abc import Sequence
@@ -78,9 +79,10 @@ class _DeviceInfos(LazyInfos):
     """infos of one device-output step, built on first access (or before the step's snapshot
     is reused) from that step's own done / truncated flags and terminal rows."""
 
-    def __init__(self, venv, slot):
+    def __init__(self, venv, slot, stamp):
         super().__init__(venv.num_envs, None)
         self._venv, self._slot = venv, slot
+        self._stamp = stamp  # Monitor's episode "t" of this step (taken when the step ran)
         self._built = None
 
     def _build(self):
@@ -95,20 +97,33 @@ class _DeviceInfos(LazyInfos):
                 idx = np.nonzero(done_h)[0]
                 ii = v.batch.torch.as_tensor(idx, device=v.batch.device)
                 tobs, ret, ln = (x.index_select(0, ii).cpu().numpy() for x in self._slot["term"])
-                done_info = v._done_dicts(idx, tobs, ret, ln, trunc.cpu().numpy())
+                done_info = v._done_dicts(idx, tobs, ret, ln, trunc.cpu().numpy(), now=self._stamp)
             self._built = v._finish_infos(done_info, self._slot["terms"])
             if v._pending and v._pending[0] is self:
                 v._pending.pop(0)
             self._slot["infos"] = None
         return self._built
 
+    def _drop(self):
+        """Discard unbuilt: the snapshot is reused; reading these infos later raises."""
+        v = self._venv
+        if self in v._pending:
+            v._pending.remove(self)
+        self._slot["infos"] = None
+        self._slot = None
+
     def __len__(self):
         return self._n
 
     def __getitem__(self, i):
+        if self._built is None and self._slot is None:
+            raise RuntimeError("the infos of this step were read after their snapshot was reused (two steps "
+                               "later); with monitor=False unread infos are not kept")
         return self._build()[i]
 
     def done_indices(self):
+        if self._built is None and self._slot is None:
+            raise RuntimeError("the infos of this step were read after their snapshot was reused")
         return self._build().done_indices()
 
 
@@ -137,6 +152,9 @@ class RocketVecEnv(_VecEnvBase):
         self.episode_lengths = []
         self.episode_times = []
         self.total_steps = 0
+        # cost split of step_wait (bench.py's SB3 legs): a dict the caller sets, accumulating
+        # seconds per stage ("launch", "kernel", "d2h", "infos"); None = no timing
+        self.timing = None
         self.cfg = self.batch.cfg
         self.state_names = self.batch.cfg.state_names if hasattr(self.batch.cfg, "state_names") else None
         if device_outputs:
@@ -158,24 +176,42 @@ class RocketVecEnv(_VecEnvBase):
         self.total_steps += self.num_envs
         if self.device_outputs:
             return self._step_device()
+        tm = self.timing
+        if tm is not None:
+            t0 = time.perf_counter()
         obs, rew, done, trunc = self.batch.step(self._actions)
+        if tm is not None:  # the kernel's remaining device time, split from the copies
+            t1 = time.perf_counter()
+            self.batch.torch.cuda.synchronize(self.batch.device)
+            t2 = time.perf_counter()
         obs_h = obs.cpu().numpy()
         rew_h = rew.cpu().numpy()
         done_h = done.cpu().numpy().astype(bool)
+        if tm is not None:
+            t3 = time.perf_counter()
         done_info = {}
         if done_h.any():
             idx, tobs, ret, ln = self.batch.fetch_done()
             done_info = self._done_dicts(idx, tobs, ret, ln, trunc.cpu().numpy())
-        return obs_h, rew_h, done_h, self._finish_infos(done_info, self.batch.terms)
+        infos = self._finish_infos(done_info, self.batch.terms)
+        if tm is not None:
+            t4 = time.perf_counter()
+            for k, v in (("launch", t1 - t0), ("kernel", t2 - t1), ("d2h", t3 - t2), ("infos", t4 - t3)):
+                tm[k] = tm.get(k, 0.0) + v
+        return obs_h, rew_h, done_h, infos
 
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
 
-    def _done_dicts(self, idx, tobs, ret, ln, trunc_h):
-        """infos of the done envs (SB3 DummyVecEnv + TimeLimit + Monitor), Monitor stats recorded."""
+    def _now(self):
+        return round(time.time() - self._t_start, 6)
+
+    def _done_dicts(self, idx, tobs, ret, ln, trunc_h, now=None):
+        """infos of the done envs (SB3 DummyVecEnv + TimeLimit + Monitor), Monitor stats recorded
+        (episode "t" = `now`, the time of the step that ended the episodes; default: now)."""
         done_info = {}
-        now = round(time.time() - self._t_start, 6)
+        now = self._now() if now is None else now
         for k, i in enumerate(np.asarray(idx).tolist()):
             d = {"terminal_observation": np.asarray(tobs[k]).copy()}
             if trunc_h[i]:
@@ -218,17 +254,31 @@ class RocketVecEnv(_VecEnvBase):
             self._pending[0]._build()
 
     def _step_device(self):
+        tm = self.timing
+        if tm is not None:
+            t0 = time.perf_counter()
         self._slot ^= 1
         st = self._sets[self._slot]
-        if st["infos"] is not None:  # its snapshot is about to be reused: build it first
-            st["infos"]._build()
+        old = st["infos"]
+        if old is not None:  # its snapshot is about to be reused
+            if self.monitor:
+                old._build()  # Monitor statistics are a side effect: every step's infos are built
+            else:
+                old._drop()  # nobody read them and building has no effect: drop unbuilt
+        if tm is not None:
+            t1 = time.perf_counter()
         obs, rew, done, trunc = self.batch.step(self._actions, out=st["out"])
-        self.batch.copy_terminal(out=st["term"])  # this step's terminal rows, device to device
+        # this step's terminal rows, device to device: only the rows of the envs done now
+        self.batch.copy_terminal(out=st["term"])
         if st["terms"] is not None:
             st["terms"].copy_(self.batch.terms)
-        infos = _DeviceInfos(self, st)
+        infos = _DeviceInfos(self, st, self._now())
         st["infos"] = infos
         self._pending.append(infos)
+        if tm is not None:  # "infos": the Monitor build of step t - 2 (incl. its done-flag copy)
+            t2 = time.perf_counter()
+            for k, v in (("infos", t1 - t0), ("launch", t2 - t1)):
+                tm[k] = tm.get(k, 0.0) + v
         return obs, rew, done.bool(), infos
 
     def close(self):

@@ -1,0 +1,99 @@
+"""bench.py's multi-rank launch contract and the EpisodeAnalyzer host logic
+(no GPU needed)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_launch_plan():
+    from bench import launch_plan
+
+    assert launch_plan(1, {}) == ("run", None)
+    assert launch_plan(2, {}) == ("spawn", None)
+    assert launch_plan(8, {}) == ("spawn", None)
+    assert launch_plan(2, {"WORLD_SIZE": "2"}) == ("run", None)
+    assert launch_plan(1, {"WORLD_SIZE": "1"}) == ("run", None)
+    plan, msg = launch_plan(8, {"WORLD_SIZE": "1"})
+    assert plan == "error" and "WORLD_SIZE" in msg
+    assert launch_plan(0, {})[0] == "error"
+
+
+def _run(args, **env):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=e, capture_output=True,
+                          text=True, timeout=300)
+
+
+def test_bench_gpus_fails_loudly_without_enough_gpus():
+    """--gpus N > visible GPUs: non-zero exit and a message, never a silent one-GPU line. (On a
+    box with >= 2 GPUs this would start ranks; the test only runs where fewer are visible.)"""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this host has >= 2 GPUs")
+    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1"])
+    assert r.returncode != 0 and "needs 2 visible GPU" in r.stderr
+    assert '"metric"' not in r.stdout
+
+
+def test_bench_gpus_must_match_world_size():
+    r = _run(["--gpus", "8"], WORLD_SIZE="1")
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
+def _stub_env(T=6):
+    from rl_rocket_amd.envs import Rocket6DOF
+    from rl_rocket_amd.params import STATE_NAMES_6DOF
+
+    u = object.__new__(Rocket6DOF)
+    u.state_names = list(STATE_NAMES_6DOF)
+    u.action_names = ["gimbal_y", "gimbal_z", "thrust"]
+    u.target_r = 30
+    u.landing_target = [0, 0, 0]
+    rng = np.random.default_rng(0)
+    states = [rng.normal(size=14) for _ in range(T + 1)]
+
+    class SIM:
+        pass
+
+    u.SIM = SIM()
+    u.SIM.states, u.SIM.actions = states, [[0, 0, 0]] + [list(rng.normal(size=3)) for _ in range(T)]
+    u.vtarg_history = [rng.normal(size=3) for _ in range(T)]
+    u.observation_space = u.action_space = None
+    return u
+
+
+def test_episode_analyzer_statistics_host():
+    sys.path.insert(0, os.path.join(ROOT, "compat"))
+    from my_environment.wrappers import EpisodeAnalyzer
+
+    u = _stub_env()
+    script = [({"rew_goal": 0.0, "attitude_constraint": 0.0}, False)] * 5 + [({"rew_goal": 10.0,
+                                                                                "attitude_constraint": 0.0}, True)]
+    it = iter(script)
+
+    def step(a):
+        rd, done = next(it)
+        return np.zeros(14, np.float32), 1.0, done, {"rewards_dict": rd}
+
+    u.step = step
+    env = EpisodeAnalyzer(u)
+    for _ in range(6):
+        env.step(np.zeros(3))
+    st = env.last_episode["stats"]
+    assert st["ep_statistic/landing_success"] == 10.0
+    np.testing.assert_allclose(st["ep_statistic/used_mass"], u.SIM.states[0][-1] - u.SIM.states[-1][-1])
+    np.testing.assert_allclose(st["final_errors/vx"], abs(u.SIM.states[-1][3]))
+    assert len(env.last_episode["rewards"]) == 6 and env.rewards_info == []
+    # the shim's figures (plotly is in this image)
+    import plotly.graph_objects as go
+
+    assert isinstance(u.get_trajectory_plotly(), go.Figure)
+    assert isinstance(u.get_vtarg_trajectory(), go.Figure)

@@ -1,4 +1,6 @@
 """GPU: the gym / SB3 surfaces over the HIP kernel (single-env shims and RocketVecEnv)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -362,3 +364,73 @@ def test_sb3_check_env_on_shims():
 
     assert check_env(_F32(env3)) == []
     env3.close()
+
+
+def test_vec_env_device_outputs_without_monitor_keeps_hbm_only():
+    """with device_outputs and monitor=False, infos nobody reads are dropped unbuilt
+    when their snapshot is reused (no done-flag copy to the host); infos read in time describe
+    their own step like the host-output twin's; infos read too late raise instead of lying."""
+    import torch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.vec_env import RocketVecEnv
+
+    n = 2048
+    dev = RocketVecEnv(n, model="6DOF", device="cuda:0", max_episode_steps=4, monitor=False, device_outputs=True,
+                       **ENV_CONFIG_6DOF)
+    host = RocketVecEnv(n, model="6DOF", device="cuda:0", max_episode_steps=4, monitor=False, **ENV_CONFIG_6DOF)
+    dev.reset()
+    host.reset()
+    rng = np.random.default_rng(3)
+    infos = []
+    for k in range(9):
+        a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+        _, _, dd, idv = dev.step(torch.from_numpy(a).cuda())
+        _, _, dh, ih = host.step(a)
+        infos.append(idv)
+        if k % 4 == 3:  # read right away (all envs hit TimeLimit 4 here)
+            assert idv.done_indices() == ih.done_indices() and len(ih.done_indices()) == n
+            for i in ih.done_indices()[:50]:
+                np.testing.assert_array_equal(idv[i]["terminal_observation"], ih[i]["terminal_observation"])
+                assert idv[i]["TimeLimit.truncated"] == ih[i]["TimeLimit.truncated"]
+    with pytest.raises(RuntimeError):
+        infos[0][0]  # its snapshot was reused at step 2 and dropped unbuilt
+    assert dev.episode_lengths == []  # no Monitor: nothing recorded
+    dev.close()
+    host.close()
+
+
+def test_episode_analyzer_drop_in():
+    """main_6DOF.make_eval_env wraps the eval env in EpisodeAnalyzer (wrappers.py:189-235): the
+    restated wrapper steps the HIP-backed shim, keeps every step's rewards_dict and, at the end
+    of the episode, the reference's statistics (final |state| per state name, landing success =
+    the last rew_goal, used mass); the shim builds the reference's plotly figures."""
+    import sys
+
+    import plotly.graph_objects as go
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "compat"))
+    from my_environment.wrappers import EpisodeAnalyzer
+    from rl_rocket_amd.envs import Rocket6DOF
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+
+    env = EpisodeAnalyzer(Rocket6DOF(device="cuda:0", **ENV_CONFIG_6DOF))
+    env.reset()
+    rng = np.random.default_rng(0)
+    steps, done = 0, False
+    while not done and steps < 1000:
+        _, _, done, info = env.step(rng.uniform(-1, 1, 3).astype(np.float32))
+        steps += 1
+    assert done
+    ep = env.last_episode
+    u = env.unwrapped
+    assert len(ep["rewards"]) == steps and env.rewards_info == []
+    assert len(ep["states"]) == steps + 1 and len(ep["vtarg"]) == steps
+    st = ep["stats"]
+    assert st["ep_statistic/landing_success"] == info["rewards_dict"]["rew_goal"]
+    np.testing.assert_allclose(st["ep_statistic/used_mass"], u.SIM.states[0][-1] - u.SIM.states[-1][-1])
+    for k, name in enumerate(u.state_names):
+        np.testing.assert_allclose(st["final_errors/" + name], abs(u.SIM.states[-1][k]))
+    assert isinstance(u.get_trajectory_plotly(), go.Figure)
+    assert isinstance(u.get_vtarg_trajectory(), go.Figure)
+    assert isinstance(u.get_attitude_trajectory(), go.Figure)
+    u.close()

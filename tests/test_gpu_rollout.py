@@ -246,20 +246,17 @@ def test_fused_collect_matches_semantics(fused, prec):
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16x3"])
 @pytest.mark.parametrize("model", [6, 3])
-@pytest.mark.parametrize("collect_nt", ["2", "1"])
-def test_one_launch_rollout_bitwise_equals_two_launch(model, prec, collect_nt, monkeypatch):
+def test_one_launch_rollout_bitwise_equals_two_launch(model, prec):
     """rr_rollout_collect (the whole rollout + GAE in one kernel) and rr_rollout_step (policy +
     env step in one kernel per step) against rr_policy_act + rr_step: every rollout buffer,
     the env outputs (incl. reward terms), the terminal rows and the env state bitwise equal
     over two collects (TimeLimit 6 < n_steps: truncation bootstraps and auto-resets inside the
-    rollout; ragged N: idle waves in the last workgroup). collect_nt: rr_rollout_collect with
-    64 (default) or 32 (RR_ROLLOUT_NT=1) envs per wave."""
+    rollout; ragged N: idle waves in the last workgroup)."""
     import torch
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
     from rl_rocket_amd.rollout import DeviceRollout
 
-    monkeypatch.setenv("RR_ROLLOUT_NT", collect_nt)
     n, T = 4096 + 37, 8
     ns, na = (14, 3) if model == 6 else (7, 2)
     kw = ENV_CONFIG_6DOF if model == 6 else {}

@@ -225,11 +225,12 @@ def test_checkpoint_restore_is_bitwise():
 @pytest.mark.parametrize("model,n,soa", [(6, 4096 + 77, False), (6, 20003, False), (6, 131072 + 5, True), (6, 65536, False),
                                          (3, 20003, True), (3, 4096 + 77, False)])
 def test_step_repeat_direct_launch_is_bitwise_step(model, n, soa):
-    """rr_step_repeat_timed (K direct launches queued behind the host-released gate kernel, two
-    timing events around them) and rr_step_repeat under stream capture: bitwise the same
-    outputs, terminal rows, Monitor returns, counter words and state as one rr_step per step,
-    across a re-seed."""
+    """bench.py's event-timed direct-launch region (tools/libbench_timed.so: K rr_step calls
+    queued behind the host-released gate kernel, two timing events around them) and
+    rr_step_repeat under stream capture: bitwise the same outputs, terminal rows, Monitor
+    returns, counter words and state as one rr_step per step, across a re-seed."""
     import torch
+    from bench import TimedLoop
     from rl_rocket_amd.batch import RocketBatch
 
     kw = _env6() if model == 6 else {}
@@ -238,6 +239,7 @@ def test_step_repeat_direct_launch_is_bitwise_step(model, n, soa):
     a, b = mk(), mk()
     a.reset()
     b.reset()
+    loop = TimedLoop(b)
     pool = torch.rand((3, n, a.action_dim), device="cuda:0", generator=torch.Generator("cuda:0").manual_seed(5)) * 2 - 1
     if soa:
         pool = pool.transpose(1, 2).contiguous()
@@ -252,7 +254,8 @@ def test_step_repeat_direct_launch_is_bitwise_step(model, n, soa):
         for t in range(chunk):
             a.step(pool[t % 3])
             resets += int(a.done.sum())
-        b.step_repeat(pool, chunk, events=ev)
+        fn, fargs = loop.call(pool, chunk, ev)
+        assert fn(*fargs) == 0
         torch.cuda.synchronize()
         assert ev[0].elapsed_time(ev[1]) > 0.0
         for x, y in ((a.obs, b.obs), (a.reward, b.reward), (a.done, b.done), (a.truncated, b.truncated),
@@ -280,3 +283,107 @@ def test_step_repeat_direct_launch_is_bitwise_step(model, n, soa):
     assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward)
     for x, y in zip(a.get_state(), b.get_state()):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("model,n,help_max", [(6, 4096 + 77, None), (6, 20003, None), (6, 20003, 0), (3, 4096 + 77, 0)])
+def test_reseed_applies_to_graphs_captured_before(model, n, help_max, monkeypatch):
+    """every kernel reads the reset-stream key from the device copy of the parameters,
+    so a hipGraph captured BEFORE rr_seed resets with the NEW key when replayed after it — with
+    helper waves (N <= RR_HELP_MAX_N: one main wave per workgroup at 4 173 envs, four at 20 003)
+    and without them (RR_HELP_MAX_N=0: the main waves draw the candidates). Replays are bitwise an
+    eager twin seeded the same way, and differ from a twin that kept the old seed."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    if help_max is not None:
+        monkeypatch.setenv("RR_HELP_MAX_N", str(help_max))
+    kw = _env6() if model == 6 else {}
+    mk = lambda: RocketBatch(n, model=model, device="cuda:0", max_episode_steps=3, **kw)  # noqa: E731
+    a, b, c = mk(), mk(), mk()
+    for e in (a, b, c):
+        e.reset()
+    acts = _actions(n, a.action_dim, 6, 21)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for act in acts:
+                b.step(act)
+    torch.cuda.current_stream().wait_stream(s)
+    a.seed(777)
+    b.seed(777)
+    g.replay()
+    for act in acts:
+        a.step(act)
+        c.step(act)
+    torch.cuda.synchronize()
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done)
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
+    assert not torch.equal(a.get_state()[0], c.get_state()[0])  # the key changed the resets
+
+
+def test_elapsed_saturates_past_the_time_limit():
+    """without auto-reset a finished env keeps stepping; its elapsed field saturates
+    at 2^E - 1 (E = 3 bits for TimeLimit 5) instead of wrapping into the episode field, so
+    TimeLimit keeps reporting done (and truncated where the physics did not end the episode),
+    as gym's TimeLimit does for every step past the limit."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 256
+    b = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=5, auto_reset=False, episode_stats=True,
+                    compute_terms=True, **_env6())
+    assert b.counter_bits == 3
+    b.reset()
+    act = torch.zeros((n, 3), device="cuda:0")
+    for t in range(1, 21):
+        obs, rew, done, trunc = b.step(act)
+        phys = (b.terms[-2] > 0.5) | (b.terms[-1] > 0.5)
+        el, ep = b.split_counter(b.checkpoint()["counter"])
+        assert bool((el == min(t, 7)).all()) and bool((ep == 1).all()), t
+        if t >= 5:
+            assert bool(done.bool().all()), t
+            assert torch.equal(trunc.bool(), ~phys), t
+        else:
+            assert torch.equal(done.bool(), phys), t
+
+
+def test_make_counter_rejects_spilling_values():
+    from rl_rocket_amd.batch import RocketBatch
+
+    b = RocketBatch(8, model=6, device="cuda:0", max_episode_steps=800, **_env6())
+    assert b.make_counter(1023, 5).view(np.uint32)[()] == (5 << 10) | 1023
+    with pytest.raises(ValueError):
+        b.make_counter(1024)
+    with pytest.raises(ValueError):
+        b.make_counter(3, 1 << 22)
+
+
+def test_copy_terminal_writes_only_the_done_rows():
+    """rr_copy_terminal copies the terminal rows of the envs done at the last step (from its
+    done masks) and leaves every other destination row untouched: the rows equal the host done
+    list of rr_fetch_done."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 4096 + 77
+    b = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=30, **_env6())
+    b.reset()
+    ck = b.checkpoint()
+    ck["counter"] = torch.as_tensor(b.make_counter(np.arange(n) % 30), device="cuda:0")
+    b.restore(ck)
+    tobs = torch.full((n, 14), float("nan"), device="cuda:0")
+    ret = torch.full((n,), -7.0, device="cuda:0")
+    ln = torch.full((n,), -1, dtype=torch.int32, device="cuda:0")
+    b.step(_actions(n, 3, 1, 2)[0])
+    b.copy_terminal(out=(tobs, ret, ln))
+    idx, to, r, l = b.fetch_done()
+    assert 0 < len(idx) < n
+    np.testing.assert_array_equal(tobs.cpu().numpy()[idx], to)
+    np.testing.assert_array_equal(ret.cpu().numpy()[idx], r)
+    np.testing.assert_array_equal(ln.cpu().numpy()[idx], l)
+    rest = np.setdiff1d(np.arange(n), idx)
+    assert np.isnan(tobs.cpu().numpy()[rest]).all()
+    assert (ret.cpu().numpy()[rest] == -7.0).all() and (ln.cpu().numpy()[rest] == -1).all()
