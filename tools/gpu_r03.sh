@@ -37,7 +37,9 @@ if has dist; then
   # sharded-step == one-batch check under torchrun
   (export RR_BENCH_ONE_DEVICE=1 RR_BENCH_BACKEND=gloo; step bench_gpus2_gloo 400 python bench.py --gpus 2 --steps 20 --warmup 5 > "$OUT/bench_gpus2_gloo.json" 2> "$OUT/bench_gpus2_gloo.err") || exit $?
   cat "$OUT/bench_gpus2_gloo.json"
-  step bench_gpus2_plain 120 python bench.py --gpus 2 --steps 20 --warmup 5 > "$OUT/bench_gpus2_plain.json" 2> "$OUT/bench_gpus2_plain.err"
+  # without the rehearsal knobs on a one-GPU box: must fail loudly (exit 2, no line), before any GPU use
+  timeout -k 10 120 python bench.py --gpus 2 --steps 20 --warmup 5 > "$OUT/bench_gpus2_plain.json" 2> "$OUT/bench_gpus2_plain.err"
+  echo "[bench_gpus2_plain] exit $? (expected 2)" | tee -a "$OUT/status.txt"
   step bench_gather_w1 300 python bench.py --gather-leg --steps 20 --warmup 5 --no-cpu-baseline --no-sb3-legs > "$OUT/bench_gather_w1.json" 2> "$OUT/bench_gather_w1.err"
   (export RR_BENCH_ONE_DEVICE=1 RR_BENCH_BACKEND=gloo; step dist_check_gloo2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29613 tools/dist_check.py > "$OUT/dist_check_gloo2.json" 2> "$OUT/dist_check_gloo2.err") || exit $?
   cat "$OUT/dist_check_gloo2.json"
