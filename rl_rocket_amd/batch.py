@@ -62,10 +62,29 @@ class RocketBatch:
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
+    def _upload(self, action):
+        """Host (numpy) actions -> the device through a persistent pinned staging buffer and an
+        asynchronous copy (pageable H2D goes through the runtime's bounce buffers, ~10x slower);
+        an event guards the staging buffer against reuse before its previous copy has run."""
+        t = self.torch
+        a = np.asarray(action, dtype=np.float32)
+        shape = (self.action_dim, self.num_envs) if self.action_soa else (self.num_envs, self.action_dim)
+        if a.size != self.num_envs * self.action_dim:
+            raise ValueError("expected %d actions, got shape %s" % (self.num_envs * self.action_dim, a.shape))
+        if getattr(self, "_stage", None) is None:
+            self._stage = (t.empty(shape, dtype=t.float32, pin_memory=True),
+                           t.empty(shape, dtype=t.float32, device=self.device), t.cuda.Event())
+        pin, dev, ev = self._stage
+        ev.synchronize()  # the previous upload has left the staging buffer
+        np.copyto(pin.numpy(), a.reshape(shape))
+        dev.copy_(pin, non_blocking=True)
+        ev.record(t.cuda.current_stream(self.device))
+        return dev
+
     def _check_action(self, action):
         t = self.torch
         if not isinstance(action, t.Tensor):
-            action = t.as_tensor(np.asarray(action, dtype=np.float32), device=self.device)
+            action = self._upload(action)
         if action.device != self.device:
             action = action.to(self.device, non_blocking=True)
         if action.dtype != t.float32:

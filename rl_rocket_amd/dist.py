@@ -5,7 +5,8 @@ collective is optional: reassembling the per-step outputs of all shards on every
 (``all_gather`` over RCCL/xGMI with the "nccl" backend), for a learner that wants the
 global batch. Ranks own envs [offset, offset + n_local); the reset stream is keyed on
 global ids, so results do not depend on the shard layout
-(tests/test_gpu_parity.py::test_sharded_stepping_is_bitwise_one_batch).
+(tests/test_gpu_state.py::test_sharded_stepping_is_bitwise_one_batch; multi-rank:
+tools/dist_check.py under torchrun, profiles/r03/).
 """
 
 

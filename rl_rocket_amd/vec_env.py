@@ -38,15 +38,44 @@ except Exception:  # pragma: no cover
     _VecEnvBase = object
 
 
-class LazyInfos(Sequence):
-    """SB3 ``infos`` list whose dicts are built on access."""
+class _DoneRows:
+    """The envs that finished at one step, as arrays (env index, terminal obs row, episode
+    return / length, truncation flag); their info dicts are built on first access."""
 
-    def __init__(self, n, done_info, terms=None, term_names=None, extra=None):
+    def __init__(self, idx, tobs, ret, ln, trunc, max_episode_steps, monitor, stamp):
+        self.idx = np.asarray(idx)
+        self.pos = dict(zip(self.idx.tolist(), range(len(self.idx))))
+        self.tobs, self.ret, self.ln, self.trunc = tobs, ret, ln, trunc
+        self.max_steps = max_episode_steps
+        self.monitor = monitor
+        self.stamp = stamp
+
+    def info(self, i):
+        """SB3 DummyVecEnv + gym TimeLimit + Monitor info of done env i (None if not done)."""
+        k = self.pos.get(i)
+        if k is None:
+            return None
+        d = {"terminal_observation": self.tobs[k]}
+        if self.trunc[k]:
+            d["TimeLimit.truncated"] = True
+        elif self.max_steps and self.ln[k] >= self.max_steps:
+            d["TimeLimit.truncated"] = False
+        if self.monitor:
+            d["episode"] = {"r": round(float(self.ret[k]), 6), "l": int(self.ln[k]), "t": self.stamp}
+        return d
+
+
+class LazyInfos(Sequence):
+    """SB3 ``infos`` list whose dicts are built on access: {} for running envs (plus
+    ``rewards_dict`` / ``bounds_violation`` with info_terms), the done envs' dicts from their
+    arrays (``_DoneRows``)."""
+
+    def __init__(self, n, done_rows=None, terms=None, term_names=None):
         self._n = n
-        self._done = done_info          # {env_idx: dict}
+        self._rows = done_rows          # _DoneRows or None
         self._terms = terms             # host [n_terms+2, N] array or None
         self._names = term_names
-        self._extra = extra or {}
+        self._cache = {}
 
     def __len__(self):
         return self._n
@@ -58,29 +87,28 @@ class LazyInfos(Sequence):
             i += self._n
         if not 0 <= i < self._n:
             raise IndexError(i)
-        d = self._done.get(i)
+        d = self._cache.get(i)
         if d is None:
-            d = {}
+            d = (self._rows.info(i) if self._rows is not None else None)
+            if d is None:
+                d = {}
             if self._terms is not None:
-                self._fill_terms(i, d)
-                self._done[i] = d
+                t = self._terms
+                d["rewards_dict"] = {k: float(t[j, i]) for j, k in enumerate(self._names)}
+                d["bounds_violation"] = bool(t[len(self._names), i] > 0.5)
+            self._cache[i] = d
         return d
 
-    def _fill_terms(self, i, d):
-        t = self._terms
-        d["rewards_dict"] = {k: float(t[j, i]) for j, k in enumerate(self._names)}
-        d["bounds_violation"] = bool(t[len(self._names), i] > 0.5)
-
     def done_indices(self):
-        return sorted(k for k, v in self._done.items() if "terminal_observation" in v)
+        return [] if self._rows is None else self._rows.idx.tolist()
 
 
 class _DeviceInfos(LazyInfos):
-    """infos of one device-output step, built on first access (or before the step's snapshot
-    is reused) from that step's own done / truncated flags and terminal rows."""
+    """infos of one device-output step, built on first access (or, with Monitor, before the
+    step's snapshot is reused) from that step's own done / truncated flags and terminal rows."""
 
     def __init__(self, venv, slot, stamp):
-        super().__init__(venv.num_envs, None)
+        super().__init__(venv.num_envs)
         self._venv, self._slot = venv, slot
         self._stamp = stamp  # Monitor's episode "t" of this step (taken when the step ran)
         self._built = None
@@ -92,13 +120,15 @@ class _DeviceInfos(LazyInfos):
                 v._pending[0]._build()
             _, _, done, trunc = self._slot["out"]
             done_h = done.cpu().numpy().astype(bool)
-            done_info = {}
+            rows = None
             if done_h.any():
-                idx = np.nonzero(done_h)[0]
+                idx = np.flatnonzero(done_h)
                 ii = v.batch.torch.as_tensor(idx, device=v.batch.device)
                 tobs, ret, ln = (x.index_select(0, ii).cpu().numpy() for x in self._slot["term"])
-                done_info = v._done_dicts(idx, tobs, ret, ln, trunc.cpu().numpy(), now=self._stamp)
-            self._built = v._finish_infos(done_info, self._slot["terms"])
+                rows = v._done_rows(idx, tobs, ret, ln, trunc.index_select(0, ii).cpu().numpy(), self._stamp)
+            terms = self._slot["terms"]
+            self._built = LazyInfos(v.num_envs, rows, None if terms is None else terms.cpu().numpy(),
+                                    v.cfg.term_names)
             if v._pending and v._pending[0] is self:
                 v._pending.pop(0)
             self._slot["infos"] = None
@@ -187,13 +217,15 @@ class RocketVecEnv(_VecEnvBase):
         obs_h = obs.cpu().numpy()
         rew_h = rew.cpu().numpy()
         done_h = done.cpu().numpy().astype(bool)
+        trunc_h = trunc.cpu().numpy()
         if tm is not None:
             t3 = time.perf_counter()
-        done_info = {}
+        rows = None
         if done_h.any():
             idx, tobs, ret, ln = self.batch.fetch_done()
-            done_info = self._done_dicts(idx, tobs, ret, ln, trunc.cpu().numpy())
-        infos = self._finish_infos(done_info, self.batch.terms)
+            rows = self._done_rows(idx, tobs, ret, ln, trunc_h[idx], self._now())
+        infos = LazyInfos(self.num_envs, rows, self.batch.terms.cpu().numpy() if self.info_terms else None,
+                          self.cfg.term_names)
         if tm is not None:
             t4 = time.perf_counter()
             for k, v in (("launch", t1 - t0), ("kernel", t2 - t1), ("d2h", t3 - t2), ("infos", t4 - t3)):
@@ -207,31 +239,14 @@ class RocketVecEnv(_VecEnvBase):
     def _now(self):
         return round(time.time() - self._t_start, 6)
 
-    def _done_dicts(self, idx, tobs, ret, ln, trunc_h, now=None):
-        """infos of the done envs (SB3 DummyVecEnv + TimeLimit + Monitor), Monitor stats recorded
-        (episode "t" = `now`, the time of the step that ended the episodes; default: now)."""
-        done_info = {}
-        now = self._now() if now is None else now
-        for k, i in enumerate(np.asarray(idx).tolist()):
-            d = {"terminal_observation": np.asarray(tobs[k]).copy()}
-            if trunc_h[i]:
-                d["TimeLimit.truncated"] = True
-            elif self.max_episode_steps and ln[k] >= self.max_episode_steps:
-                d["TimeLimit.truncated"] = False
-            if self.monitor:
-                d["episode"] = {"r": round(float(ret[k]), 6), "l": int(ln[k]), "t": now}
-                self.episode_returns.append(float(ret[k]))
-                self.episode_lengths.append(int(ln[k]))
-                self.episode_times.append(now)
-            done_info[i] = d
-        return done_info
-
-    def _finish_infos(self, done_info, terms_dev):
-        terms = terms_dev.cpu().numpy() if self.info_terms else None
-        if terms is not None:
-            for i, d in done_info.items():
-                LazyInfos._fill_terms(LazyInfos(0, {}, terms, self.cfg.term_names), i, d)
-        return LazyInfos(self.num_envs, done_info, terms, self.cfg.term_names)
+    def _done_rows(self, idx, tobs, ret, ln, trunc_k, now):
+        """The done envs of a step (SB3 DummyVecEnv + TimeLimit + Monitor); Monitor statistics
+        recorded here, vectorised (episode "t" = `now`, the time of the step that ended them)."""
+        if self.monitor:
+            self.episode_returns.extend(ret.tolist())
+            self.episode_lengths.extend(ln.tolist())
+            self.episode_times.extend([now] * len(idx))
+        return _DoneRows(idx, tobs, ret, ln, trunc_k, self.max_episode_steps, self.monitor, now)
 
     # -- device outputs: double-buffered step outputs + per-step snapshots for the lazy infos ---------------
     def _init_device_sets(self):

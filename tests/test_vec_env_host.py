@@ -37,16 +37,16 @@ def test_done_infos_match_sb3_semantics():
     env = _env()
     trunc = np.array([0, 1, 0, 0, 0], np.uint8)
     idx, tobs, ret, ln = env.batch.fetch_done()
-    infos = env._finish_infos(env._done_dicts(idx, tobs, ret, ln, trunc), None)
+    infos = LazyInfos(5, env._done_rows(idx, tobs, ret, ln, trunc[idx], 1.5), None, ["a"])
     assert len(infos) == 5
     assert infos[0] == {} and infos[2] == {} and infos[4] == {}
     assert infos[1]["TimeLimit.truncated"] is True
     assert "TimeLimit.truncated" not in infos[3]
     np.testing.assert_array_equal(infos[3]["terminal_observation"], np.arange(14, 28, dtype=np.float32))
-    assert infos[1]["episode"]["r"] == -12.5 and infos[1]["episode"]["l"] == 800
+    assert infos[1]["episode"]["r"] == -12.5 and infos[1]["episode"]["l"] == 800 and infos[1]["episode"]["t"] == 1.5
     assert infos[3]["episode"]["l"] == 42
     assert infos.done_indices() == [1, 3]
-    assert env.episode_lengths == [800, 42]
+    assert env.episode_lengths == [800, 42] and env.episode_returns == [-12.5, 3.25] and env.episode_times == [1.5] * 2
     # SB3 VecNormalize mutates done infos in place: the mutation must persist
     infos[1]["terminal_observation"] = "x"
     assert infos[1]["terminal_observation"] == "x"
@@ -55,6 +55,6 @@ def test_done_infos_match_sb3_semantics():
 
 def test_lazy_infos_terms():
     terms = np.array([[1.0, 2.0], [0.0, 1.0], [0.0, 0.0]])
-    li = LazyInfos(2, {}, terms, ["velocity_tracking"])
+    li = LazyInfos(2, None, terms, ["velocity_tracking"])
     assert li[0] == {"rewards_dict": {"velocity_tracking": 1.0}, "bounds_violation": False}
     assert li[1]["bounds_violation"] is True
