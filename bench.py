@@ -529,41 +529,54 @@ def sb3_legs(dev, n, steps):
 # ---------------------------------------------------------------------------------------------
 # committed evidence of the same kernel source (rocprofv3 PMC traffic, kernel-trace durations)
 # ---------------------------------------------------------------------------------------------
-def _stored(pattern, model, n, want_hash):
+_ISA = {}
+
+
+def _isa_hashes():
+    """ISA hash per kernel of the library this process runs (rl_rocket_amd.build.kernel_isa_hashes)."""
+    if not _ISA:
+        from rl_rocket_amd import build as B
+        try:
+            _ISA.update(B.kernel_isa_hashes(B.OUT))
+        except Exception as e:  # noqa: BLE001 - tools missing: quote nothing
+            _ISA["__error__"] = str(e)
+    return _ISA
+
+
+def _stored(pattern, model, n):
+    """The newest committed profile file matching `pattern` for this kernel and N whose kernel
+    machine code (isa_hash of its kernel_name) is the code this process runs; else (None, reason)."""
     import glob
 
     hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", pattern % n), recursive=True),
                   key=os.path.getmtime)
+    isa = _isa_hashes()
     stale = None
     for path in reversed(hits):
         with open(path) as f:
             d = json.load(f)
         if not d.get("kernel", "").startswith("step_kernel<%d," % model):
             continue
-        if d.get("source_hash") == want_hash:
+        if d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]:
             return d, os.path.relpath(path, ROOT)
         stale = stale or os.path.relpath(path, ROOT)
-    return None, ("no file for kernel source %s (latest, other source: %s)" % (want_hash, stale))
+    return None, ("no file measured on this kernel's machine code (latest, other code: %s)%s"
+                  % (stale, "; " + isa["__error__"] if "__error__" in isa else ""))
 
 
 def stored_traffic(model, n):
     """Per-launch HBM bytes of the same kernel/config from the latest committed rocprofv3 PMC
     passes (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), only if they were measured on
-    THIS kernel code (same rl_rocket_amd.build.source_hash); else (None, reason)."""
-    from rl_rocket_amd.build import source_hash
-
-    d, src = _stored("pmc_traffic_n%d.json", model, n, source_hash())
+    THIS kernel's machine code (same ISA hash); else (None, reason)."""
+    d, src = _stored("pmc_traffic_n%d.json", model, n)
     return (d["traffic_bytes"], src) if d else (None, src)
 
 
 def stored_rocprof(model, n, steps):
     """The step kernel's rocprofv3 kernel-trace mean of the same protocol (tools/rocprof_step.py:
     a --kernel-trace --stats run of this bench command, committed under profiles/), only if it
-    was measured on THIS kernel code; else (None, reason)."""
-    from rl_rocket_amd.build import source_hash
-
-    d, src = _stored("rocprof_step_k%d_n%%d.json" % steps, model, n, source_hash())
-    return d, src
+    was measured on THIS kernel's machine code; else (None, reason)."""
+    return _stored("rocprof_step_k%d_n%%d.json" % steps, model, n)
 
 
 def main():

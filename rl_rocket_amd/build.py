@@ -58,6 +58,66 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
+def _llvm(tool):
+    for d in (os.environ.get("ROCM_PATH", "/opt/rocm") + "/lib/llvm/bin", "/opt/rocm/llvm/bin"):
+        if os.path.exists(os.path.join(d, tool)):
+            return os.path.join(d, tool)
+    found = shutil.which(tool)
+    if not found:
+        raise RuntimeError("%s not found" % tool)
+    return found
+
+
+def _elf_symbols(blob):
+    """(name, bytes) of the FUNC symbols and kernel descriptors (OBJECT *.kd) of an ELF64 blob."""
+    import struct
+
+    shoff, = struct.unpack_from("<Q", blob, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", blob, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", blob, shoff + i * shentsize) for i in range(shnum)]
+    out = {}
+    for sec in secs:
+        if sec[1] != 2:  # SHT_SYMTAB
+            continue
+        strtab = secs[sec[6]]
+        for k in range(sec[5] // 24):
+            name_off, info, _other, shndx, value, size = struct.unpack_from("<IBBHQQ", blob, sec[4] + 24 * k)
+            if size == 0 or shndx == 0 or shndx >= len(secs) or (info & 0xF) not in (1, 2):  # OBJECT / FUNC
+                continue
+            so = strtab[4] + name_off
+            name = blob[so:blob.index(b"\0", so)].decode()
+            tsec = secs[shndx]
+            start = tsec[4] + (value - tsec[3])
+            out[name] = blob[start:start + size]
+    return out
+
+
+def kernel_isa_hashes(lib=OUT):
+    """{demangled kernel name: sha256[:16] of its gfx950 machine code + kernel descriptor} of
+    a built library: the identity of the code a profile measured, independent of unrelated
+    edits elsewhere in the translation unit (bench.py quotes committed PMC / rocprofv3 figures
+    only for the same ISA). Uses llvm-objcopy, clang-offload-bundler (ROCm) and c++filt."""
+    import hashlib
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "dev.co")
+        subprocess.check_call([_llvm("llvm-objcopy"), "--dump-section=.hip_fatbin=" + fat, lib, os.path.join(d, "x")])
+        subprocess.check_call([_llvm("clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + fat,
+                               "--targets=hipv4-amdgcn-amd-amdhsa--%s" % ARCH, "--output=" + co])
+        with open(co, "rb") as f:
+            syms = _elf_symbols(f.read())
+    funcs = sorted(n for n in syms if not n.endswith(".kd"))
+    names = subprocess.run(["c++filt"], input="\n".join(funcs), capture_output=True, text=True,
+                           check=True).stdout.splitlines()
+    out = {}
+    for mangled, name in zip(funcs, names):
+        h = hashlib.sha256(syms[mangled])
+        h.update(syms.get(mangled + ".kd", b""))
+        out[name] = h.hexdigest()[:16]
+    return out
+
+
 def up_to_date():
     if not os.path.exists(OUT):
         return False

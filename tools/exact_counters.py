@@ -1,0 +1,74 @@
+"""Counter summary of the exact-mode kernel (step_exact_kernel / step_exact_pair_kernel) from the
+rocprofv3 passes of tools/gpu_r03.sh (exact_kt: kernel trace; exact_SQ, exact_SQ2: --pmc).
+
+    python tools/exact_counters.py gpurun_out/<tag> [--out profiles/r03/<tag>/exact_counters.json]
+
+Per dispatch medians, per-wave figures and the shares of wave cycles (SQ_WAVE_CYCLES and the
+SQ_WAIT / SQ_ACTIVE counters count quad-cycles: x4 for cycles, MI355X_MICROARCH.md).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def counters(d):
+    out = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "step_exact" not in r["Kernel_Name"]:
+                continue
+            out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in out.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run_dir")
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    c = {}
+    for sub in ("exact_SQ", "exact_SQ2"):
+        c.update(counters(os.path.join(a.run_dir, sub)))
+    res = {"median_per_dispatch": c}
+    stats = glob.glob(os.path.join(a.run_dir, "exact_kt", "**", "*kernel_stats.csv"), recursive=True)
+    for f in stats:
+        for r in csv.DictReader(open(f)):
+            if "step_exact" in r["Name"]:
+                res["kernel_trace"] = {"name": r["Name"], "calls": int(r["Calls"]), "mean_us": float(r["AverageNs"]) / 1e3,
+                                       "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3}
+    bench = os.path.join(a.run_dir, "bench_exact.json")
+    if os.path.exists(bench):
+        line = [json.loads(x) for x in open(bench) if x.startswith("{")][-1]
+        res["bench"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
+                        "kernel_us_events": line["roofline"]["kernel_us"], "n": line["config"]["envs_per_gpu"]}
+    w = c.get("SQ_WAVES")
+    if w:
+        d = {}
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                  "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_SALU", "SQ_INSTS_VMEM", "SQ_INSTS_BRANCH", "SQ_INSTS_SMEM"):
+            if k in c:
+                d[k + "_per_wave"] = c[k] / w
+        for k in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+            if k in c:
+                d[k + "_cycles_per_wave"] = 4 * c[k] / w
+        wc = c.get("SQ_WAVE_CYCLES")
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+            if k in c and wc:
+                d[k + "_share_of_wave_cycles"] = c[k] / wc
+        if "SQ_INSTS_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
+            d["valu_cycles_per_valu_inst"] = 4 * c["SQ_ACTIVE_INST_VALU"] / c["SQ_INSTS_VALU"]
+        res["derived"] = d
+    res["source"] = a.run_dir
+    text = json.dumps(res, indent=1)
+    print(text)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        with open(a.out, "w") as f:
+            f.write(text + "\n")
+
+
+if __name__ == "__main__":
+    main()

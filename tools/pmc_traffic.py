@@ -14,18 +14,24 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def median_counter(d, name):
+STEP = re.compile(r"(?<![A-Za-z_])step_kernel<")
+
+
+def median_counter(d, name, names=None):
     f = glob.glob(os.path.join(d, "pmc_%s" % name, "*counter_collection.csv"))
     if not f:
         return None
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f[0]))
-            if "step_kernel" in r["Kernel_Name"] and r["Counter_Name"] == name]
+    rows = [r for r in csv.DictReader(open(f[0])) if STEP.search(r["Kernel_Name"]) and r["Counter_Name"] == name]
+    if names is not None:
+        names.update(r["Kernel_Name"] for r in rows)
+    vals = [float(r["Counter_Value"]) for r in rows]
     return statistics.median(vals) if vals else None
 
 
@@ -36,12 +42,18 @@ def main():
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--model", type=int, default=6)
     a = ap.parse_args()
-    fetch = median_counter(a.run_dir, "FETCH_SIZE")
-    write = median_counter(a.run_dir, "WRITE_SIZE")
+    names = set()
+    fetch = median_counter(a.run_dir, "FETCH_SIZE", names)
+    write = median_counter(a.run_dir, "WRITE_SIZE", names)
+    if len(names) != 1:
+        raise SystemExit("expected one step_kernel instantiation in the passes, got %s" % sorted(names))
+    from rl_rocket_amd.build import kernel_isa_hashes
+    kname = names.pop()
     loaded = {6: 76, 3: 44}[a.model] * a.n
     stored = {6: 122, 3: 66}[a.model] * a.n
     res = {
         "kernel": "step_kernel<%d,RK4>" % a.model, "n": a.n,
+        "kernel_name": kname, "isa_hash": kernel_isa_hashes().get(kname),
         "fetch_size_kib": fetch, "write_size_kib": write,
         "read_bytes": 2 * fetch * 1024, "write_bytes": write * 1024,
         "traffic_bytes": 2 * fetch * 1024 + write * 1024,

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--bench", help="bench JSON line file (default: RUN_DIR/bench.json)")
     ap.add_argument("--out")
     a = ap.parse_args()
-    from rl_rocket_amd.build import source_hash
+    from rl_rocket_amd.build import kernel_isa_hashes, source_hash
 
     bench = a.bench or os.path.join(a.run_dir, "bench.json")
     with open(bench) as f:
@@ -48,6 +48,7 @@ def main():
     res = {
         "kernel": "step_kernel<%d,%s>" % (model, line["config"]["integrator"].upper()),
         "kernel_name": row["Name"],
+        "isa_hash": kernel_isa_hashes().get(row["Name"]),
         "n": line["config"]["envs_per_gpu"], "steps": line["steps"], "warmup": line["warmup"],
         "launch": line["config"]["launch"],
         "calls": int(row["Calls"]), "mean_ns": mean, "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"]),
