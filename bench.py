@@ -60,12 +60,14 @@ def parse(argv=None):
                     help="the drop-in default (RocketVecEnv monitor=True): Monitor running return kept per env "
                          "(read + written every step, +8 B per env-step); the headline runs without it")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--launch", default="auto", choices=["auto", "graph", "loop"],
+    ap.add_argument("--launch", default="auto", choices=["auto", "graph", "loop", "isolated"],
                     help="graph: K launches replayed from hipGraphs; loop: K direct launches of rr_step issued back "
                          "to back from C (tools/libbench_timed.so, action batch t mod 8 of the resident pool, the HIP "
                          "events recorded around them); auto: loop for K < %d, else graph (a graph replay carries "
                          "a fixed ~8 us preamble on the GPU timeline, a direct launch ~0.3 us more than a "
-                         "graph-captured one: DESIGN.md section 5)" % AUTO_LOOP_MAX_K)
+                         "graph-captured one: DESIGN.md section 5); isolated: one launch at a time, each between "
+                         "its own pair of HIP events and followed by a host synchronize (kernel_us = the mean "
+                         "isolated launch, the regime of a step between a policy's kernels)" % AUTO_LOOP_MAX_K)
     ap.add_argument("--graph-steps", type=int, default=1024,
                     help="env steps captured per hipGraph (each replay costs a fixed ~15-20 us on the GPU "
                          "timeline: 64 -> 4.34 us/step, 256 -> 4.25, 1024 -> 4.18 at N=65536)")
@@ -194,6 +196,30 @@ def timed_region(args, env, pool, dev, dist, backend, launch, gather=None):
 
     use_loop = launch == "loop" and gather is None
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if launch == "isolated":
+        for k in range(args.warmup):
+            one(k)
+        torch.cuda.synchronize(dev)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(K):
+            evs[k][0].record(stream)
+            one(k)
+            evs[k][1].record(stream)
+            torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        per = sorted(a.elapsed_time(b) for a, b in evs)
+        if dist is not None:
+            t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return {"dt": dt, "kern_ms": sum(per) / K, "use_graph": False, "use_loop": False, "gs": 0,
+                "isolated_median_ms": per[K // 2], "isolated_min_ms": per[0]}
     loop = TimedLoop(env) if use_loop else None
     if use_loop:
         ev0.record(stream)
@@ -652,7 +678,7 @@ def main():
     bytes_launch = bytes_env * n
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     achieved_wall = bytes_launch / (dt / K) / 1e9
-    headline_cfg = not (args.monitor or args.allgather or args.integrator != "rk4")
+    headline_cfg = not (args.monitor or args.allgather or args.integrator != "rk4" or launch == "isolated")
     if headline_cfg:
         traffic, traffic_src = stored_traffic(model, n)
         rp, rp_src = stored_rocprof(model, n, K)
@@ -694,7 +720,9 @@ def main():
                                   "no data-path collective") + (", Monitor returns" if args.monitor else ""),
                    "envs_per_gpu": n, "global_envs": n * world, "integrator": args.integrator,
                    "graph_steps": reg["gs"] if reg["use_graph"] else 0, "launch": "graph" if reg["use_graph"] else
-                   ("direct: tools/libbench_timed.so (K rr_step calls)" if reg["use_loop"] else "rr_step per step"),
+                   ("direct: tools/libbench_timed.so (K rr_step calls)" if reg["use_loop"] else
+                    "isolated: one rr_step between two HIP events + synchronize per step" if launch == "isolated" else
+                    "rr_step per step"),
                    "parallelism": "env-sharded x%d" % world,
                    "world_size": dist.get_world_size() if dist is not None else 1,
                    "backend": dist.get_backend() if dist is not None else None},
@@ -721,10 +749,13 @@ def main():
     }
 
     # ---- the step + all_gather leg (reported separately from the step alone) ----
+    if launch == "isolated":
+        result["roofline"]["isolated_median_us"] = reg["isolated_median_ms"] * 1e3
+        result["roofline"]["isolated_min_us"] = reg["isolated_min_ms"] * 1e3
     if gather_leg:
         from rl_rocket_amd.dist import ShardGather
         g = ShardGather(n, env.state_dim, dev)
-        greg = timed_region(args, env, pool, dev, dist, backend, "graph" if launch == "loop" else launch, g)
+        greg = timed_region(args, env, pool, dev, dist, backend, "graph" if launch in ("loop", "isolated") else launch, g)
         result["allgather"] = {
             "value": n * world * K / greg["dt"], "unit": "env-steps/s", "ms_per_step": greg["dt"] / K * 1e3,
             "device_us_per_step": greg["kern_ms"] * 1e3,
