@@ -1459,6 +1459,7 @@ struct rr_env {
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
     KParams* d_kp;      // device copy of kp (Bufs.kp)
+    XParams* d_xp;      // device copy of xp (RR_INT_DOPRI5: step_exact_kernel reads it where it uses it)
     int32_t* g_idx;     // rr_fetch_done scratch
     float* g_obs;
     float* g_ret;
@@ -1577,6 +1578,8 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->kp.id_off = env_id_offset;
     {
         hipError_t err = hipMalloc((void**)&e->d_kp, sizeof(KParams));
+        if (err == hipSuccess) err = hipMalloc((void**)&e->d_xp, sizeof(XParams));
+        if (err == hipSuccess) err = hipMemcpy(e->d_xp, &e->xp, sizeof(XParams), hipMemcpyHostToDevice);
         if (err != hipSuccess) {
             rr_destroy(e);
             return hip_fail(err, "rr_create: hipMalloc (params)");
@@ -1599,7 +1602,7 @@ int rr_destroy(rr_env* e)
 {
     if (!e) return RR_OK;
     DeviceGuard g(e->device);
-    void* ptrs[] = {e->state, e->state64, e->d_kp, e->done_bits,
+    void* ptrs[] = {e->state, e->state64, e->d_kp, e->d_xp, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -1664,8 +1667,8 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     const bool euler = e->p.integrator == RR_INT_EULER;
     const dim3 grid(grid_of(e->n)), block(kBlock);
     if (e->p.integrator == RR_INT_DOPRI5) {
-        if (m6) hipLaunchKernelGGL(step_exact_kernel<6>, grid, block, 0, s, e->kp, e->xp, b, io, e->state64);
-        else hipLaunchKernelGGL(step_exact_kernel<3>, grid, block, 0, s, e->kp, e->xp, b, io, e->state64);
+        if (m6) hipLaunchKernelGGL(step_exact_kernel<6>, grid, block, 0, s, e->d_xp, b, io, e->state64);
+        else hipLaunchKernelGGL(step_exact_kernel<3>, grid, block, 0, s, e->d_xp, b, io, e->state64);
     } else {
         const uint32_t nn = (uint32_t)e->n;
         const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
