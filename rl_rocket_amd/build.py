@@ -113,7 +113,9 @@ def kernel_isa_hashes(lib=OUT):
     out = {}
     for mangled, name in zip(funcs, names):
         h = hashlib.sha256(syms[mangled])
-        h.update(syms.get(mangled + ".kd", b""))
+        kd = bytearray(syms.get(mangled + ".kd", b""))
+        kd[16:24] = bytes(8)[:len(kd[16:24])]  # kernel_code_entry_byte_offset: where the code sits, not what it is
+        h.update(bytes(kd))
         out[name] = h.hexdigest()[:16]
     return out
 
