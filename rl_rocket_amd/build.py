@@ -10,7 +10,13 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "rocket_hip.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc", "rocket_rollout.inc")]
+# the exact-mode kernels' translation unit (rocket_hip.hip again under RR_TU_EXACT), compiled with
+# a register-pressure-first scheduler: with the fast kernels' setting the 6DOF exact kernel spilled
+# 33 VGPRs to scratch at one wave per SIMD (r03e), with it none
+SRC_EXACT = os.path.join(HERE, "csrc", "rocket_exact.hip")
+EXACT_FLAGS = ["-mllvm", "-amdgpu-schedule-metric-bias=100"]
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc", "rocket_rollout.inc",
+                                                 "rocket_exact.hip")]
 HEADER = os.path.join(ROOT, "include", "rocket_hip.h")
 OUT = os.path.join(HERE, "librocket_hip.so")
 # benchmark-only helper (not part of the product ABI): bench.py's event-timed direct-launch region
@@ -26,7 +32,7 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def command(resource_usage=False, out=OUT, defines=(), extra=()):
+def command(resource_usage=False, out=OUT, defines=(), extra=(), src=SRC, compile_only=False):
     # -fno-slp-vectorize: the SLP pass packs scalar f32 math into v_pk_* pairs and adds ~180
     # register moves to the step kernel (measured on the .s); the scalar stream is shorter.
     # -ffp-contract=on: a*b+c becomes an fma only inside one source expression. HIP's default
@@ -36,9 +42,9 @@ def command(resource_usage=False, out=OUT, defines=(), extra=()):
     # contraction makes every kernel that inlines the physics compute the same bits.
     # kernarg preload: the step kernel's leading pointer / word arguments arrive in user SGPRs
     cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-fno-slp-vectorize", "-ffp-contract=on", "-std=c++17",
-           "-fPIC", "-shared", "-mllvm", "-amdgpu-kernarg-preload-count=4",
+           "-fPIC", "-c" if compile_only else "-shared", "-mllvm", "-amdgpu-kernarg-preload-count=4",
            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")] + list(extra) + \
-        ["-D%s" % d for d in defines] + ["-o", out, SRC]
+        ["-D%s" % d for d in defines] + ["-o", out, src]
     if resource_usage:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     return cmd
@@ -54,8 +60,35 @@ def source_hash():
     for path in [SRC, HEADER] + DEPS:
         with open(path, "rb") as f:
             h.update(f.read())
-    h.update(" ".join(command()[1:-1]).replace(ROOT, "").encode())
+    for cmd in commands():
+        h.update(" ".join(cmd[1:]).replace(ROOT, "").encode())
     return h.hexdigest()[:16]
+
+
+def commands(resource_usage=False, out=OUT, defines=(), extra=()):
+    """The three steps of the library build: the main translation unit and the exact-mode one
+    compiled to objects (the latter with EXACT_FLAGS), then linked into `out`."""
+    o_main, o_exact = out + ".main.o", out + ".exact.o"
+    c1 = command(resource_usage, o_main, defines, extra, SRC, compile_only=True)
+    c2 = command(resource_usage, o_exact, defines, list(extra) + EXACT_FLAGS, SRC_EXACT, compile_only=True)
+    c3 = [hipcc(), "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-o", out, o_main, o_exact]
+    return [c1, c2, c3]
+
+
+def build_lib(out=OUT, defines=(), extra=(), resource_usage=False, verbose=True):
+    """Compile both translation units (in parallel) and link `out`."""
+    c1, c2, c3 = commands(resource_usage, out, defines, extra)
+    if verbose:
+        for c in (c1, c2, c3):
+            print("[rl_rocket_amd.build]", " ".join(c), flush=True)
+    procs = [subprocess.Popen(c, cwd=ROOT) for c in (c1, c2)]
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs, key=abs), c1 if rcs[0] else c2)
+    subprocess.check_call(c3, cwd=ROOT)
+    for o in (c1[c1.index("-o") + 1], c2[c2.index("-o") + 1]):
+        os.remove(o)
+    return out
 
 
 def _llvm(tool):
@@ -100,13 +133,26 @@ def kernel_isa_hashes(lib=OUT):
     import hashlib
     import tempfile
 
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    syms = {}
     with tempfile.TemporaryDirectory() as d:
-        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "dev.co")
+        fat = os.path.join(d, "fat.bin")
         subprocess.check_call([_llvm("llvm-objcopy"), "--dump-section=.hip_fatbin=" + fat, lib, os.path.join(d, "x")])
-        subprocess.check_call([_llvm("clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + fat,
-                               "--targets=hipv4-amdgcn-amd-amdhsa--%s" % ARCH, "--output=" + co])
-        with open(co, "rb") as f:
-            syms = _elf_symbols(f.read())
+        with open(fat, "rb") as f:
+            blob = f.read()
+        starts, k = [], blob.find(magic)  # one bundle per translation unit
+        while k >= 0:
+            starts.append(k)
+            k = blob.find(magic, k + len(magic))
+        for n, k0 in enumerate(starts):
+            k1 = starts[n + 1] if n + 1 < len(starts) else len(blob)
+            part, co = os.path.join(d, "b%d.bin" % n), os.path.join(d, "b%d.co" % n)
+            with open(part, "wb") as f:
+                f.write(blob[k0:k1])
+            subprocess.check_call([_llvm("clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + part,
+                                   "--targets=hipv4-amdgcn-amd-amdhsa--%s" % ARCH, "--output=" + co])
+            with open(co, "rb") as f:
+                syms.update(_elf_symbols(f.read()))
     funcs = sorted(n for n in syms if not n.endswith(".kd"))
     names = subprocess.run(["c++filt"], input="\n".join(funcs), capture_output=True, text=True,
                            check=True).stdout.splitlines()
@@ -131,11 +177,7 @@ def build(force=False, resource_usage=False, verbose=True):
     build_bench_helper(force=force, verbose=verbose)
     if not force and up_to_date():
         return OUT
-    cmd = command(resource_usage)
-    if verbose:
-        print("[rl_rocket_amd.build]", " ".join(cmd), flush=True)
-    subprocess.check_call(cmd, cwd=ROOT)
-    return OUT
+    return build_lib(OUT, resource_usage=resource_usage, verbose=verbose)
 
 
 def build_bench_helper(force=False, verbose=True):

@@ -1064,6 +1064,7 @@ __device__ __forceinline__ void store_outputs(const StepIO& io, uint32_t i, uint
 // ROWS (rr_step_rows): obs, reward and done leave as ONE row of NS + 2 fp32 per env
 // (obs[NS], reward, done as 0 / 1) through the same LDS tile, e.g. straight into the send
 // buffer of the multi-GPU all-gather (rl_rocket_amd.dist.ShardGather).
+#ifndef RR_TU_EXACT  // rocket_exact.hip compiles this file again for the exact-mode kernels only
 template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB, bool ROWS>
 __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR void step_kernel(
     float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
@@ -1283,12 +1284,45 @@ __global__ __launch_bounds__(kBlock) void copy_done_rows_kernel(const uint64_t* 
 // On-device PPO rollout kernels (fused MlpPolicy forward on fp32 MFMA, bootstrap, GAE)
 #include "rocket_policy.inc"
 #include "rocket_rollout.inc"
+#endif  // RR_TU_EXACT
 
 // Exact-integrator mode (RR_INT_DOPRI5): fp64 scipy RK45 restatement, compiled without
-// FMA contraction so its roundings follow the reference's numpy arithmetic.
+// FMA contraction so its roundings follow the reference's numpy arithmetic. Its kernels are
+// compiled in the second translation unit (rocket_exact.hip); this one keeps XParams and the
+// fp32 <-> fp64 plane conversions.
 #pragma clang fp contract(off)
 #include "rocket_dopri5.inc"
 #pragma clang fp contract(fast)
+
+#ifdef RR_TU_EXACT
+}  // namespace
+
+// the exact TU's only entry point (hidden: not part of the C-ABI). bufs / io / xp point to the
+// Bufs / StepIO / XParams of the calling TU (same definitions, same layout).
+extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model, const void* xp, const void* bufs,
+                                                                        const void* io, double* state64,
+                                                                        unsigned grid, void* stream)
+{
+    Bufs b;
+    StepIO o;
+    std::memcpy(&b, bufs, sizeof(Bufs));
+    std::memcpy(&o, io, sizeof(StepIO));
+    const XParams* x = static_cast<const XParams*>(xp);
+    if (model == RR_MODEL_6DOF)
+        hipLaunchKernelGGL(step_exact_kernel<6>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, x, b, o, state64);
+    else
+        hipLaunchKernelGGL(step_exact_kernel<3>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, x, b, o, state64);
+    return (int)hipGetLastError();
+}
+#else  // the main translation unit: host side
+
+// defined by the exact translation unit; this weak stand-in (a library built from this file alone,
+// e.g. a tools/ A/B variant) makes RR_INT_DOPRI5 steps fail loudly instead of failing to load
+extern "C" __attribute__((weak, visibility("hidden"))) int rrx_launch_exact(int, const void*, const void*,
+                                                                          const void*, double*, unsigned, void*)
+{
+    return (int)hipErrorInvalidDeviceFunction;
+}
 
 // ---------------------------------------------------------------------------
 // Host side
@@ -1667,8 +1701,11 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     const bool euler = e->p.integrator == RR_INT_EULER;
     const dim3 grid(grid_of(e->n)), block(kBlock);
     if (e->p.integrator == RR_INT_DOPRI5) {
-        if (m6) hipLaunchKernelGGL(step_exact_kernel<6>, grid, block, 0, s, e->d_xp, b, io, e->state64);
-        else hipLaunchKernelGGL(step_exact_kernel<3>, grid, block, 0, s, e->d_xp, b, io, e->state64);
+        // the exact kernels live in the second translation unit (rocket_exact.hip: compiled with a
+        // register-pressure-first scheduler, no scratch spills)
+        const hipError_t xe = (hipError_t)rrx_launch_exact(m6 ? RR_MODEL_6DOF : RR_MODEL_3DOF, e->d_xp, &b, &io,
+                                                           e->state64, grid.x, s);
+        if (xe != hipSuccess) return hip_fail(xe, "rr_step: exact launch");
     } else {
         const uint32_t nn = (uint32_t)e->n;
         const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
@@ -2188,3 +2225,4 @@ int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, cons
 
 
 }  // extern "C"
+#endif  // RR_TU_EXACT
