@@ -605,6 +605,22 @@ def stored_rocprof(model, n, steps):
     return _stored("rocprof_step_k%d_n%%d.json" % steps, model, n)
 
 
+def gather_leg_result(args, env, pool, dev, dist, backend, launch, n, world, K):
+    """The step + all_gather leg (reported separately from the step alone)."""
+    from rl_rocket_amd.dist import ShardGather
+
+    g = ShardGather(n, env.state_dim, dev)
+    greg = timed_region(args, env, pool, dev, dist, backend, "graph" if launch in ("loop", "isolated") else launch, g)
+    return {
+        "value": n * world * K / greg["dt"], "unit": "env-steps/s", "ms_per_step": greg["dt"] / K * 1e3,
+        "device_us_per_step": greg["kern_ms"] * 1e3,
+        "world_size": dist.get_world_size(), "backend": dist.get_backend(),
+        "bytes_per_rank_per_step": g.n_pad * (env.state_dim + 2) * 4,
+        "launch": "graph" if greg["use_graph"] else "eager (gloo stages through the host)",
+        "what": "rr_step_rows into the send rows + ONE all_gather_into_tensor of [N][state_dim+2] fp32 rows "
+                "(obs, reward, done) per step, the global batch on every rank (ShardGather.step)"}
+
+
 def main():
     args = parse()
     plan, msg = launch_plan(args.gpus, os.environ)
@@ -636,11 +652,15 @@ def main():
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
     if world > 1 or args.allgather or gather_leg:
+        import datetime
+
         import torch.distributed as dist
+        # a rank that dies must not leave the others waiting in a collective for the default 10 min
+        tmo = datetime.timedelta(seconds=int(os.environ.get("RR_BENCH_PG_TIMEOUT", "180")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
         world = dist.get_world_size()
 
     from rl_rocket_amd.batch import RocketBatch
@@ -753,17 +773,12 @@ def main():
         result["roofline"]["isolated_median_us"] = reg["isolated_median_ms"] * 1e3
         result["roofline"]["isolated_min_us"] = reg["isolated_min_ms"] * 1e3
     if gather_leg:
-        from rl_rocket_amd.dist import ShardGather
-        g = ShardGather(n, env.state_dim, dev)
-        greg = timed_region(args, env, pool, dev, dist, backend, "graph" if launch in ("loop", "isolated") else launch, g)
-        result["allgather"] = {
-            "value": n * world * K / greg["dt"], "unit": "env-steps/s", "ms_per_step": greg["dt"] / K * 1e3,
-            "device_us_per_step": greg["kern_ms"] * 1e3,
-            "world_size": dist.get_world_size(), "backend": dist.get_backend(),
-            "bytes_per_rank_per_step": g.n_pad * (env.state_dim + 2) * 4,
-            "launch": "graph" if greg["use_graph"] else "eager (gloo stages through the host)",
-            "what": "rr_step_rows into the send rows + ONE all_gather_into_tensor of [N][state_dim+2] fp32 rows "
-                    "(obs, reward, done) per step, the global batch on every rank (ShardGather.step)"}
+        # failures are reported in the line, never at the expense of the step-only headline (the
+        # process group's timeout bounds any wait on a rank that failed first)
+        try:
+            result["allgather"] = gather_leg_result(args, env, pool, dev, dist, backend, launch, n, world, K)
+        except Exception as e:  # noqa: BLE001
+            result["allgather"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baselines(model, args.cpu_seconds, host_cores())
     env.close()
