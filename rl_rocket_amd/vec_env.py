@@ -119,13 +119,7 @@ class _DeviceInfos(LazyInfos):
             while v._pending and v._pending[0] is not self:  # earlier steps first (Monitor order)
                 v._pending[0]._build()
             _, _, done, trunc = self._slot["out"]
-            done_h = done.cpu().numpy().astype(bool)
-            rows = None
-            if done_h.any():
-                idx = np.flatnonzero(done_h)
-                ii = v.batch.torch.as_tensor(idx, device=v.batch.device)
-                tobs, ret, ln = (x.index_select(0, ii).cpu().numpy() for x in self._slot["term"])
-                rows = v._done_rows(idx, tobs, ret, ln, trunc.index_select(0, ii).cpu().numpy(), self._stamp)
+            rows = v._gather_done(done, trunc, self._slot["term"], self._stamp)
             terms = self._slot["terms"]
             self._built = LazyInfos(v.num_envs, rows, None if terms is None else terms.cpu().numpy(),
                                     v.cfg.term_names)
@@ -263,6 +257,37 @@ class RocketVecEnv(_VecEnvBase):
             })
         self._slot = 0
         self._pending = []  # unbuilt _DeviceInfos in step order
+        pin = dict(pin_memory=True)
+        self._gbuf = {"done": t.empty((n,), dtype=t.uint8, **pin), "idx_h": t.empty((n,), dtype=t.int64, **pin),
+                      "idx_d": t.empty((n,), dtype=t.int64, device=dev)}
+        for key, shape, dt in (("obs", (n, ns), t.float32), ("ret", (n,), t.float32), ("len", (n,), t.int32),
+                               ("trunc", (n,), t.uint8)):
+            self._gbuf[key + "_d"] = t.empty(shape, dtype=dt, device=dev)
+            self._gbuf[key + "_h"] = t.empty(shape, dtype=dt, **pin)
+
+    def _gather_done(self, done, trunc, term, stamp):
+        """The done envs of a device-output step as host arrays, through preallocated device /
+        pinned buffers (no allocation per step): done flags D2H, the done rows gathered on the
+        device (index_select into fixed buffers), one copy of each to the host, one sync."""
+        t = self.batch.torch
+        g = self._gbuf
+        g["done"].copy_(done)
+        idx = np.flatnonzero(g["done"].numpy())
+        m = len(idx)
+        if not m:
+            return None
+        g["idx_h"][:m].copy_(t.from_numpy(idx))
+        ii = g["idx_d"][:m]
+        ii.copy_(g["idx_h"][:m], non_blocking=True)
+        outs = []
+        for src, key in zip(tuple(term) + (trunc,), ("obs", "ret", "len", "trunc")):
+            dev, host = g[key + "_d"][:m], g[key + "_h"][:m]
+            t.index_select(src, 0, ii, out=dev)
+            host.copy_(dev, non_blocking=True)
+            outs.append(host)
+        t.cuda.current_stream(self.batch.device).synchronize()
+        tobs, ret, ln, tr = (h.numpy().copy() for h in outs)  # the pinned buffers are reused next step
+        return self._done_rows(idx, tobs, ret, ln, tr, stamp)
 
     def _flush_all(self):
         while self._pending:
