@@ -493,9 +493,9 @@ def sb3_legs(dev, n, steps):
     venv = RocketVecEnv(n, model="6DOF", device=dev, max_episode_steps=MAX_EPISODE_STEPS, monitor=True,
                         **ENV_CONFIG_6DOF)
     venv.reset()
-    run(venv, host_pool, 0, 10)
+    run(venv, host_pool, 0, 30)
     t0 = time.perf_counter()
-    n_done = run(venv, host_pool, 10, steps)
+    n_done = run(venv, host_pool, 30, steps)
     dt = time.perf_counter() - t0
     venv.timing = {}
     run(venv, host_pool, 0, steps)
@@ -510,25 +510,30 @@ def sb3_legs(dev, n, steps):
                       "(rr_fetch_done) + terminal_observation / TimeLimit.truncated / Monitor dicts of the done envs",
         "path": "RocketVecEnv(monitor=True).step(numpy actions) -> numpy obs/reward/done + lazy infos (SB3 VecEnv)"}
 
-    # device outputs: device actions in, device tensors out (obs stay in HBM), Monitor on
+    # device outputs: device actions in, device tensors out (obs stay in HBM); with Monitor (every
+    # step's infos built two steps later) and without (nothing leaves HBM unless read). 60 warm-up
+    # steps: the first device-output steps pay one-time pinned-buffer / allocator costs
     pool = torch.rand((POOL, n, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(1)) * 2 - 1
-    venv = RocketVecEnv(n, model="6DOF", device=dev, max_episode_steps=MAX_EPISODE_STEPS, monitor=True,
-                        device_outputs=True, **ENV_CONFIG_6DOF)
-    venv.reset()
-    run(venv, pool, 0, 10, host=False)
-    t0 = time.perf_counter()
-    run(venv, pool, 10, steps, host=False)
-    dt = time.perf_counter() - t0
-    venv.timing = {}
-    run(venv, pool, 0, steps, host=False)
-    split = {k: v / steps * 1e6 for k, v in venv.timing.items()}
-    venv.close()
-    out["vecenv_device"] = {
-        "value": n * steps / dt, "unit": "env-steps/s", "us_per_step": dt / steps * 1e6, "n_envs": n, "steps": steps,
-        "split_us_per_step": split,
-        "split_note": "launch = rr_step + the done rows' terminal copy (host time of the async calls); infos = the "
-                      "Monitor build of step t-2's infos (done-flag D2H, which waits for the GPU, + dicts)",
-        "path": "RocketVecEnv(monitor=True, device_outputs=True).step(device actions) -> device tensors + lazy infos"}
+    for mon in (True, False):
+        venv = RocketVecEnv(n, model="6DOF", device=dev, max_episode_steps=MAX_EPISODE_STEPS, monitor=mon,
+                            device_outputs=True, **ENV_CONFIG_6DOF)
+        venv.reset()
+        run(venv, pool, 0, 60, host=False)
+        t0 = time.perf_counter()
+        run(venv, pool, 60, steps, host=False)
+        dt = time.perf_counter() - t0
+        venv.timing = {}
+        run(venv, pool, 0, steps, host=False)
+        split = {k: v / steps * 1e6 for k, v in venv.timing.items()}
+        venv.close()
+        out["vecenv_device" + ("" if mon else "_no_monitor")] = {
+            "value": n * steps / dt, "unit": "env-steps/s", "us_per_step": dt / steps * 1e6, "n_envs": n,
+            "steps": steps, "split_us_per_step": split,
+            "split_note": "launch = rr_step + the done rows' terminal copy (host time of the async calls); infos = "
+                          "the Monitor build of step t-2's infos (done-flag D2H, which waits for the GPU, + the done "
+                          "rows' gather)" if mon else "launch = rr_step + the done rows' terminal copy; nothing else",
+            "path": "RocketVecEnv(monitor=%s, device_outputs=True).step(device actions) -> device tensors + lazy "
+                    "infos" % mon}
 
     # the single-env gym shim: one env, one launch + one packed D2H per step
     env = Rocket6DOF(device=dev, **ENV_CONFIG_6DOF)
