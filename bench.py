@@ -77,6 +77,10 @@ def parse(argv=None):
                     help="skip the wall-clock legs through the Python boundary (RocketVecEnv.step with host and "
                          "device outputs, the single-env gym Rocket6DOF.step)")
     ap.add_argument("--sb3-steps", type=int, default=100)
+    ap.add_argument("--n-sweep", default="4096,524288",
+                    help="other envs-per-GPU points of the north star's N in {4k, 64k, 512k}, timed with the same "
+                         "protocol (K steps after W warm-up, max over ranks) and reported in the line's n_sweep "
+                         "(empty: none)")
     ap.add_argument("--mode", default="step", choices=["step", "rollout"],
                     help="step: the fused env step (headline); rollout: on-device PPO rollout "
                          "collection (MlpPolicy 64x64 forward + sample + env step + buffer), BASELINE configs[4]")
@@ -784,9 +788,27 @@ def main():
             result["allgather"] = gather_leg_result(args, env, pool, dev, dist, backend, launch, n, world, K)
         except Exception as e:  # noqa: BLE001
             result["allgather"] = {"error": "%s: %s" % (type(e).__name__, e)}
+    env.close()
+    sweep = [int(x) for x in args.n_sweep.split(",") if x.strip()] if args.mode == "step" and not args.allgather else []
+    if sweep:
+        result["n_sweep"] = []
+        for n_i in sweep:
+            e_i = RocketBatch(n_i, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
+                              episode_stats=args.monitor, integrator=args.integrator, env_id_offset=rank * n_i, **kw)
+            e_i.reset()
+            g_i = torch.Generator(device=dev)
+            g_i.manual_seed(42 + rank)
+            p_i = torch.rand((POOL, n_i, e_i.action_dim), device=dev, generator=g_i) * 2 - 1
+            r_i = timed_region(args, e_i, p_i, dev, dist, backend, launch)
+            b_i = bytes_env * n_i
+            result["n_sweep"].append({
+                "envs_per_gpu": n_i, "global_envs": n_i * world, "value": n_i * world * K / r_i["dt"],
+                "ms_per_step": r_i["dt"] / K * 1e3, "kernel_us": r_i["kern_ms"] * 1e3,
+                "frac": b_i / (r_i["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "frac_wall": b_i / (r_i["dt"] / K) / 1e9 / HBM_PEAK_GBS})
+            e_i.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baselines(model, args.cpu_seconds, host_cores())
-    env.close()
     if rank == 0 and world == 1 and model == 6 and not args.no_sb3_legs and args.integrator == "rk4":
         result["sb3_legs"] = sb3_legs(dev, n, args.sb3_steps)
     if rank == 0:
