@@ -214,9 +214,9 @@ def timed_region(args, env, pool, dev, dist, backend, launch, gather=None):
             one(k)
             evs[k][1].record(stream)
             torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
         if dist is not None:
             dist.barrier()
-        dt = time.perf_counter() - t0
         per = sorted(a.elapsed_time(b) for a, b in evs)
         if dist is not None:
             t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
@@ -283,9 +283,11 @@ def timed_region(args, env, pool, dev, dist, backend, launch, gather=None):
                 one(k)
         ev1.record(stream)
     torch.cuda.synchronize(dev)
+    # each rank's own synchronize-to-synchronize time; the closing barrier (whose latency grows with
+    # the rank count) stays outside it, and the max over ranks below covers any straggler
+    dt = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-    dt = time.perf_counter() - t0
     if use_loop and rc != 0:
         raise RuntimeError("bt_step_repeat_timed failed: %d" % rc)
     # device time per launch over the timed region (kernel + inter-kernel gap: an upper bound
