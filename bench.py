@@ -311,7 +311,7 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
 
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import MAX_EPISODE_STEPS
-    from rl_rocket_amd.rollout import DeviceRollout, MlpActorCritic, ppo_update
+    from rl_rocket_amd.rollout import DeviceRollout, GraphedPPOUpdate, MlpActorCritic, ppo_update
 
     torch.manual_seed(42)
     env = RocketBatch(n, model=model, device=dev, max_episode_steps=MAX_EPISODE_STEPS, auto_reset=True,
@@ -350,13 +350,48 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     steps = reps * args.rollout_steps
-    opt = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    # one policy replica per GPU: minibatch gradients averaged over the ranks (one all_reduce)
-    stats = ppo_update(pol, opt, ro, n_epochs=1, batch_size=n, group=dist.group.WORLD if dist is not None else None)
-    torch.cuda.synchronize(dev)
-    upd = time.perf_counter() - t1
+    # The PPO update (SB3 1.6 PPO.train on the device-resident rollout, batch_size = N: n_steps
+    # minibatches per epoch; one policy replica per GPU, minibatch gradients averaged over the
+    # ranks with one all_reduce): eager PyTorch (one warm-up epoch, then one timed epoch) and the
+    # minibatch step captured in one hipGraph (GraphedPPOUpdate), then the end-to-end training
+    # iteration of configs[4]: one collect + SB3's default n_epochs = 10 graphed epochs.
+    opt = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5, capturable=True)
+    grp = dist.group.WORLD if dist is not None else None
+
+    def timed(fn):
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t1, out
+
+    ppo_update(pol, opt, ro, n_epochs=1, batch_size=n, group=grp)
+    upd, stats = timed(lambda: ppo_update(pol, opt, ro, n_epochs=1, batch_size=n, group=grp))
+    update = {"minibatches_per_epoch": args.rollout_steps, "batch_size": n, "eager_epoch_ms": upd * 1e3}
+    train = None
+    if dist is None or dist.get_backend() == "nccl":
+        gu = GraphedPPOUpdate(pol, opt, ro, batch_size=n, group=grp)
+        gu.update(n_epochs=1)
+        gupd, stats = timed(lambda: gu.update(n_epochs=10))
+        update["graphed_epoch_ms"] = gupd * 1e3 / 10
+        iters = 3
+
+        def train_loop():
+            for _ in range(iters):
+                g.replay()
+                gu.update(n_epochs=10)
+
+        if dist is not None:
+            dist.barrier()
+        tt, _ = timed(train_loop)
+        if dist is not None:
+            t = torch.tensor([tt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tt = float(t.item())
+        train = {"value": iters * args.rollout_steps * n * world / tt, "unit": "env-steps/s",
+                 "ms_per_iteration": tt / iters * 1e3,
+                 "what": "one training iteration = one collect (n_steps x N env-steps, one hipGraph) + 10 PPO epochs "
+                         "of graphed minibatch updates (SB3 1.6 defaults: n_epochs 10), batch_size N"}
     env.close()
     return {
         "metric": "env-steps/sec of on-device PPO rollout collection (%s, N=%d per GPU)"
@@ -375,7 +410,7 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
                     "one launch per step: rr_rollout_step (policy on %s MFMA + env step)" if ro.one_launch else
                     "two launches per step: rr_policy_act (%s MFMA) + rr_step") % args.policy_dtype},
         "gpu_ms_per_collect": e0.elapsed_time(e1) / reps,
-        "ppo_epoch_ms": upd * 1e3, "ppo_stats": stats,
+        "ppo_update": update, "ppo_stats": stats, "train_iteration": train,
     }
 
 

@@ -443,3 +443,101 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
             optimizer.step()
             stats = {"policy_loss": pg.detach(), "value_loss": vf.detach(), "entropy": -ent.detach()}
     return {k: float(v) for k, v in stats.items()}
+
+
+class GraphedPPOUpdate:
+    """``ppo_update``'s minibatch step — gather, forward, clipped-surrogate / value / entropy
+    loss, backward, (multi-GPU gradient all_reduce), grad-norm clip, Adam step — captured ONCE
+    into a hipGraph and replayed per minibatch: the ~80 small launches and their Python driving
+    become one graph launch (the update of configs[4] is otherwise host-bound: a 64x64 MLP on
+    65 536 samples is a few microseconds of device work per kernel).
+
+    Needs an optimizer created with ``capturable=True`` (``torch.optim.Adam(..., capturable=True)``:
+    its step count lives on the device) and ``n_steps * num_envs`` divisible by ``batch_size``.
+    The warm-up steps the capture requires run on the real parameters and are undone (parameters
+    and optimizer state restored in place), so the first ``update`` starts from the same state
+    as the eager ``ppo_update`` would, and computes the same minibatch steps (same kernels, same
+    order; ``tests/test_gpu_rollout.py``). Multi-GPU: ``group`` must be an RCCL ("nccl") group —
+    the all_reduce is captured with the rest."""
+
+    def __init__(self, policy, optimizer, ro, batch_size=65536, clip_range=0.2, ent_coef=0.01, vf_coef=0.5,
+                 max_grad_norm=0.5, group=None):
+        if not all(g.get("capturable", False) for g in optimizer.param_groups):
+            raise ValueError("GraphedPPOUpdate needs an optimizer with capturable=True")
+        n = ro.n_steps * ro.env.num_envs
+        if n % batch_size:
+            raise ValueError("n_steps * num_envs (%d) must be a multiple of batch_size (%d)" % (n, batch_size))
+        if group is not None:
+            import torch.distributed as dist
+            if dist.get_backend(group) != "nccl":
+                raise ValueError("a captured gradient all_reduce needs the nccl (RCCL) backend")
+        self.policy, self.optimizer, self.ro, self.group = policy, optimizer, ro, group
+        self.n, self.bs = n, batch_size
+        dev = ro.obs.device
+        self.obs = ro.obs.reshape(n, -1)
+        self.act = ro.actions.reshape(n, -1)
+        self.old_lp = ro.log_probs.reshape(n)
+        self.adv_all = ro.advantages.reshape(n)
+        self.ret = ro.returns.reshape(n)
+        self.coef = (clip_range, ent_coef, vf_coef, max_grad_norm)
+        self.idx = torch.arange(batch_size, device=dev)
+        params = list(policy.parameters())
+        # state to restore after the warm-up steps (in place: the graph keeps these tensors)
+        saved_p = [p.detach().clone() for p in params]
+        saved_s = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in optimizer.state[p].items()}
+                   for p in params if p in optimizer.state}
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                optimizer.zero_grad(set_to_none=True)
+                self._step()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        optimizer.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.stats = self._step()
+        with torch.no_grad():
+            for p, v in zip(params, saved_p):
+                p.copy_(v)
+            for p in params:
+                st = optimizer.state.get(p)
+                if not st:
+                    continue
+                old = saved_s.get(id(p))
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        if old is not None and k in old:
+                            v.copy_(old[k])
+                        else:
+                            v.zero_()  # state the warm-up created: back to a fresh optimizer's
+        torch.cuda.synchronize(dev)
+
+    def _step(self):
+        clip_range, ent_coef, vf_coef, max_grad_norm = self.coef
+        pol, i = self.policy, self.idx
+        mean, value = pol(self.obs[i])
+        lp = pol.log_prob(mean, self.act[i])
+        adv = self.adv_all[i]
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        ratio = torch.exp(lp - self.old_lp[i])
+        pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip_range, 1 + clip_range)).mean()
+        vf = torch.nn.functional.mse_loss(self.ret[i], value)
+        ent = -pol.entropy(self.bs).mean()
+        loss = pg + ent_coef * ent + vf_coef * vf
+        loss.backward()
+        if self.group is not None:
+            _allreduce_grads(list(pol.parameters()), self.group)
+        torch.nn.utils.clip_grad_norm_(pol.parameters(), max_grad_norm)
+        self.optimizer.step()
+        return {"policy_loss": pg.detach(), "value_loss": vf.detach(), "entropy": -ent.detach()}
+
+    def update(self, n_epochs=10, generator=None):
+        """n_epochs passes over the rollout in shuffled minibatches (ppo_update's order:
+        one torch.randperm per epoch)."""
+        for _ in range(n_epochs):
+            perm = torch.randperm(self.n, device=self.obs.device, generator=generator)
+            for s in range(0, self.n, self.bs):
+                self.idx.copy_(perm[s:s + self.bs])
+                self.graph.replay()
+        return {k: float(v) for k, v in self.stats.items()}

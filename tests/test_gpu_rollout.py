@@ -354,3 +354,39 @@ def test_unfused_bootstrap_ignores_stale_terminal_rows():
     ro.collect()
     assert torch.isfinite(ro.rewards).all() and torch.isfinite(ro.advantages).all()
     env.close()
+
+
+def test_graphed_ppo_update_equals_eager():
+    """GraphedPPOUpdate (the minibatch update captured once in a hipGraph, replayed per
+    minibatch) against the eager ppo_update from the same parameters, optimizer state, rollout
+    and shuffling: the same parameters after two epochs (same kernels in the same order), and the
+    capture's warm-up steps leave no trace."""
+    import copy
+
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout, GraphedPPOUpdate, ppo_update
+
+    n, T, bs = 8192, 8, 8192
+    env = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=30, **ENV_CONFIG_6DOF)
+    pol = _policy(14, 3, seed=7)
+    ro = DeviceRollout(env, pol, n_steps=T, seed=3)
+    ro.collect()
+    torch.cuda.synchronize()
+    pa, pb = copy.deepcopy(pol), copy.deepcopy(pol)
+    oa = torch.optim.Adam(pa.parameters(), lr=3e-4, eps=1e-5, capturable=True)
+    ob = torch.optim.Adam(pb.parameters(), lr=3e-4, eps=1e-5, capturable=True)
+    g = GraphedPPOUpdate(pb, ob, ro, batch_size=bs)
+    for x, y in zip(pa.parameters(), pb.parameters()):  # warm-up undone
+        assert torch.equal(x, y)
+    sa = ppo_update(pa, oa, ro, n_epochs=2, batch_size=bs, generator=torch.Generator("cuda:0").manual_seed(5))
+    sb = g.update(n_epochs=2, generator=torch.Generator("cuda:0").manual_seed(5))
+    torch.cuda.synchronize()
+    worst = max((x - y).abs().max().item() for x, y in zip(pa.parameters(), pb.parameters()))
+    moved = max((x - y).abs().max().item() for x, y in zip(pol.parameters(), pb.parameters()))
+    assert moved > 0  # the update did something
+    assert worst <= 1e-6, worst
+    for k in sa:
+        assert abs(sa[k] - sb[k]) <= 1e-5 * max(1.0, abs(sa[k])), (k, sa[k], sb[k])
+    env.close()
