@@ -20,6 +20,42 @@ import torch
 from torch import nn
 
 
+class _LinearFn(torch.autograd.Function):
+    """``F.linear`` whose bias gradient is a GEMM with a row of ones instead of a column sum.
+
+    On PyTorch 2.10 / ROCm 7 a hipGraph that runs a GEMM and then a column sum (``sum(0)``) of a
+    tensor produced in the same graph returns a wrong sum from its second replay on (the first
+    replay and eager runs are right; ``tools/probe_graph_reduce.py``: errors of 10^2 on sums of
+    ~10^3 at 8 192 and 65 536 rows, the GEMM output itself correct, the same sum as
+    ``ones @ g`` correct). A Linear's bias gradient is exactly that column sum of the output
+    gradient, so GraphedPPOUpdate's replays trained with wrong hidden-layer bias gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = g @ w
+        if ctx.needs_input_grad[1]:
+            gw = g2.t() @ x.reshape(-1, x.shape[-1])
+        if ctx.needs_input_grad[2]:
+            gb = (g2.new_ones(1, g2.shape[0]) @ g2)[0]
+        return gx, gw, gb
+
+
+class _Linear(nn.Linear):
+    """nn.Linear (same parameters, initialisation and packing) through _LinearFn."""
+
+    def forward(self, x):
+        return _LinearFn.apply(x, self.weight, self.bias)
+
+
 class MlpActorCritic(nn.Module):
     def __init__(self, obs_dim, act_dim, hidden=(64, 64), log_std_init=0.0):
         super().__init__()
@@ -28,13 +64,13 @@ class MlpActorCritic(nn.Module):
         def mlp():
             layers, d = [], obs_dim
             for h in hidden:
-                layers += [nn.Linear(d, h), nn.Tanh()]
+                layers += [_Linear(d, h), nn.Tanh()]
                 d = h
             return nn.Sequential(*layers)
 
         self.pi_net, self.vf_net = mlp(), mlp()
-        self.action_net = nn.Linear(hidden[-1], act_dim)
-        self.value_net = nn.Linear(hidden[-1], 1)
+        self.action_net = _Linear(hidden[-1], act_dim)
+        self.value_net = _Linear(hidden[-1], 1)
         self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std_init)))
         for net in (self.pi_net, self.vf_net):
             for m in net:
@@ -486,14 +522,20 @@ class GraphedPPOUpdate:
         saved_p = [p.detach().clone() for p in params]
         saved_s = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in optimizer.state[p].items()}
                    for p in params if p in optimizer.state}
+        # static gradient buffers (allocated outside the graph): the captured step copies
+        # torch.autograd.grad's results into them, so no accumulation into .grad is captured. The
+        # policy's Linear layers must take their bias gradient as a GEMM (_LinearFn): a column sum
+        # after a GEMM in the same graph is wrong from the second replay on (tools/dbg_graphed_update.py,
+        # tools/probe_graph_reduce.py)
+        self.params = params
+        for p in params:
+            p.grad = torch.zeros_like(p)
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(3):
-                optimizer.zero_grad(set_to_none=True)
                 self._step()
         torch.cuda.current_stream(dev).wait_stream(s)
-        optimizer.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.stats = self._step()
@@ -525,9 +567,10 @@ class GraphedPPOUpdate:
         vf = torch.nn.functional.mse_loss(self.ret[i], value)
         ent = -pol.entropy(self.bs).mean()
         loss = pg + ent_coef * ent + vf_coef * vf
-        loss.backward()
+        for p, g in zip(self.params, torch.autograd.grad(loss, self.params)):
+            p.grad.copy_(g)
         if self.group is not None:
-            _allreduce_grads(list(pol.parameters()), self.group)
+            _allreduce_grads(self.params, self.group)
         torch.nn.utils.clip_grad_norm_(pol.parameters(), max_grad_norm)
         self.optimizer.step()
         return {"policy_loss": pg.detach(), "value_loss": vf.detach(), "entropy": -ent.detach()}
