@@ -353,8 +353,9 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
     # The PPO update (SB3 1.6 PPO.train on the device-resident rollout, batch_size = N: n_steps
     # minibatches per epoch; one policy replica per GPU, minibatch gradients averaged over the
     # ranks with one all_reduce): eager PyTorch (one warm-up epoch, then one timed epoch) and the
-    # minibatch step captured in one hipGraph (GraphedPPOUpdate), then the end-to-end training
-    # iteration of configs[4]: one collect + SB3's default n_epochs = 10 graphed epochs.
+    # minibatch step captured in one hipGraph (GraphedPPOUpdate) with PyTorch autograd and with
+    # the rr_ppo_grad pipeline, then the end-to-end training iteration of configs[4]: one collect
+    # + SB3's default n_epochs = 10 graphed epochs.
     opt = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5, capturable=True)
     grp = dist.group.WORLD if dist is not None else None
 
@@ -370,10 +371,17 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
     update = {"minibatches_per_epoch": args.rollout_steps, "batch_size": n, "eager_epoch_ms": upd * 1e3}
     train = None
     if dist is None or dist.get_backend() == "nccl":
-        gu = GraphedPPOUpdate(pol, opt, ro, batch_size=n, group=grp)
+        gt = GraphedPPOUpdate(pol, opt, ro, batch_size=n, group=grp, fused=False)
+        gt.update(n_epochs=1)
+        gupd, _ = timed(lambda: gt.update(n_epochs=3))
+        update["graphed_epoch_ms"] = gupd * 1e3 / 3
+        del gt
+        # the loss + backward from rr_ppo_grad (fp32-MFMA HIP pipeline) instead of autograd
+        gu = GraphedPPOUpdate(pol, opt, ro, batch_size=n, group=grp, fused=True)
         gu.update(n_epochs=1)
         gupd, stats = timed(lambda: gu.update(n_epochs=10))
-        update["graphed_epoch_ms"] = gupd * 1e3 / 10
+        update["fused_graphed_epoch_ms"] = gupd * 1e3 / 10
+        update["fused_ms_per_minibatch"] = gupd * 1e3 / 10 / args.rollout_steps
         iters = 3
 
         def train_loop():
@@ -391,7 +399,8 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
         train = {"value": iters * args.rollout_steps * n * world / tt, "unit": "env-steps/s",
                  "ms_per_iteration": tt / iters * 1e3,
                  "what": "one training iteration = one collect (n_steps x N env-steps, one hipGraph) + 10 PPO epochs "
-                         "of graphed minibatch updates (SB3 1.6 defaults: n_epochs 10), batch_size N"}
+                         "of graphed minibatch updates (SB3 1.6 defaults: n_epochs 10), batch_size N, loss + "
+                         "backward by rr_ppo_grad"}
     env.close()
     return {
         "metric": "env-steps/sec of on-device PPO rollout collection (%s, N=%d per GPU)"

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 7
+#define RR_ABI_VERSION 8
 
 /* error codes */
 #define RR_OK 0
@@ -303,6 +303,27 @@ int rr_rollout_collect(rr_env* e, const float* params, int precision, uint64_t s
 int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, const float* starts,
            const float* last_value, const float* last_done, float gamma, float lam, float* advantages,
            float* returns, void* stream);
+
+/* ---- PPO minibatch gradient (the learner half of configs[4]) ----
+ * Replaces the loss + loss.backward() of stable_baselines3 1.6 PPO.train for the MlpPolicy
+ * actor-critic the reference trains (PPO("MlpPolicy", env, ..., ent_coef=0.01),
+ * main_6DOF.py:62-69; SB3 defaults otherwise): for the minibatch idx[0 .. batch) of a device
+ * rollout (obs [*][obs_dim], actions [*][act_dim], old_log_prob, advantages, returns [*]),
+ *   A = (adv - mean) / (std + 1e-8) (unbiased std), r = exp(log_prob - old_log_prob),
+ *   loss = -mean(min(A r, A clamp(r, 1 - clip_range, 1 + clip_range)))
+ *          + ent_coef * -sum(0.5 + 0.5 log(2 pi) + log_std) + vf_coef * mean((returns - V)^2),
+ * the gradient of loss with respect to the 13 parameter tensors (params / grads: HOST arrays of
+ * device fp32 pointers in rr_policy_pack's order and PyTorch layouts) is WRITTEN to grads (not
+ * accumulated). stats (device, 5 floats, or NULL): policy_loss, value_loss, entropy,
+ * clip_fraction, approx_kl (SB3's logged quantities). Deterministic (fixed-order sums, no
+ * atomics); fp32 MFMA, so the gradients equal PyTorch's autograd ones to fp32 summation-order
+ * rounding. Four launches on `stream`, capturable in a graph. Supported (obs_dim, act_dim):
+ * (14, 3), (7, 2); batch >= 2. workspace: device, 16-B aligned, rr_ppo_workspace_size bytes. */
+int rr_ppo_workspace_size(int obs_dim, int act_dim, int64_t batch, int64_t* bytes);
+int rr_ppo_grad(int obs_dim, int act_dim, const float* const* params, float* const* grads, const float* obs,
+                const float* actions, const float* old_log_prob, const float* advantages, const float* returns,
+                const int64_t* idx, int64_t batch, float clip_range, float ent_coef, float vf_coef, float* stats,
+                void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,7 @@ SRC = os.path.join(HERE, "csrc", "rocket_hip.hip")
 # 33 VGPRs to scratch at one wave per SIMD (r03e), with it none
 SRC_EXACT = os.path.join(HERE, "csrc", "rocket_exact.hip")
 EXACT_FLAGS = ["-mllvm", "-amdgpu-schedule-metric-bias=100"]
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc", "rocket_rollout.inc",
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc", "rocket_rollout.inc", "rocket_ppo.inc",
                                                  "rocket_exact.hip")]
 HEADER = os.path.join(ROOT, "include", "rocket_hip.h")
 OUT = os.path.join(HERE, "librocket_hip.so")

@@ -25,6 +25,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "rocket_hip.h"
@@ -1284,6 +1285,8 @@ __global__ __launch_bounds__(kBlock) void copy_done_rows_kernel(const uint64_t* 
 // On-device PPO rollout kernels (fused MlpPolicy forward on fp32 MFMA, bootstrap, GAE)
 #include "rocket_policy.inc"
 #include "rocket_rollout.inc"
+// PPO minibatch gradient (loss + backward of the MlpPolicy on fp32 MFMA)
+#include "rocket_ppo.inc"
 #endif  // RR_TU_EXACT
 
 // Exact-integrator mode (RR_INT_DOPRI5): fp64 scipy RK45 restatement, compiled without
@@ -2221,6 +2224,70 @@ int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, cons
                        T, n, rewards, values, starts, last_value, last_done, gamma, lam, advantages, returns);
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_gae: launch");
+}
+
+namespace {
+int64_t ppo_nwg(int64_t batch)
+{
+    const int64_t tiles = (batch + ppo::kTile - 1) / ppo::kTile;
+    const int64_t w = (tiles + ppo::kWaves - 1) / ppo::kWaves;
+    return w < 1 ? 1 : (w > ppo::kMaxWG ? ppo::kMaxWG : w);
+}
+
+int64_t ppo_part_floats(int obs_dim, int act_dim)
+{
+    if (obs_dim == 14 && act_dim == 3) return ppo::Part<14, 3>::SIZE;
+    if (obs_dim == 7 && act_dim == 2) return ppo::Part<7, 2>::SIZE;
+    return 0;
+}
+}  // namespace
+
+int rr_ppo_workspace_size(int obs_dim, int act_dim, int64_t batch, int64_t* bytes)
+{
+    const int64_t pf = ppo_part_floats(obs_dim, act_dim);
+    if (!pf) return fail(RR_EINVAL, "rr_ppo_workspace_size: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+    if (batch < 2 || !bytes) return fail(RR_EINVAL, "rr_ppo_workspace_size: batch >= 2 and bytes required");
+    *bytes = (int64_t)(2 * ppo::kAdvPart * sizeof(double)) + 2 * ppo_nwg(batch) * pf * (int64_t)sizeof(float);
+    return RR_OK;
+}
+
+int rr_ppo_grad(int obs_dim, int act_dim, const float* const* params, float* const* grads, const float* obs,
+                const float* actions, const float* old_log_prob, const float* advantages, const float* returns,
+                const int64_t* idx, int64_t batch, float clip_range, float ent_coef, float vf_coef, float* stats,
+                void* workspace, int64_t workspace_bytes, void* stream)
+{
+    int64_t need = 0;
+    const int rc = rr_ppo_workspace_size(obs_dim, act_dim, batch, &need);
+    if (rc != RR_OK) return rc;
+    if (!params || !grads || !obs || !actions || !old_log_prob || !advantages || !returns || !idx || !workspace)
+        return fail(RR_EINVAL, "rr_ppo_grad: null argument");
+    if (workspace_bytes < need) return fail(RR_EINVAL, "rr_ppo_grad: workspace smaller than rr_ppo_workspace_size");
+    if (((uintptr_t)workspace & 15) != 0) return fail(RR_EINVAL, "rr_ppo_grad: workspace must be 16-B aligned");
+    if (!(clip_range >= 0.0f)) return fail(RR_EINVAL, "rr_ppo_grad: clip_range must be >= 0");
+    PolSrc ps;
+    PolGrad pg;
+    for (int k = 0; k < 13; ++k) {
+        if (!params[k] || !grads[k]) return fail(RR_EINVAL, "rr_ppo_grad: null parameter or gradient tensor");
+        ps.p[k] = params[k];
+        pg.p[k] = grads[k];
+    }
+    hipStream_t s = (hipStream_t)stream;
+    double* adv_part = (double*)workspace;
+    float* part = (float*)((char*)workspace + 2 * ppo::kAdvPart * sizeof(double));
+    const int nwg = (int)ppo_nwg(batch);
+    hipLaunchKernelGGL(ppo_adv_kernel, dim3(ppo::kAdvPart), dim3(256), 0, s, advantages, idx, batch, adv_part);
+    auto run = [&](auto obs_c, auto act_c) {
+        constexpr int O = decltype(obs_c)::value, A = decltype(act_c)::value;
+        using PT = ppo::Part<O, A>;
+        hipLaunchKernelGGL((ppo_grad_kernel<O, A>), dim3(nwg, 2), dim3(ppo::kThreads), 0, s, ps, obs, actions,
+                           old_log_prob, advantages, returns, idx, batch, clip_range, vf_coef, adv_part, part);
+        hipLaunchKernelGGL((ppo_finish_kernel<O, A>), dim3((PT::SIZE + 63) / 64, 2), dim3(256), 0, s, part, nwg, batch,
+                           ent_coef, ps, pg, stats);
+    };
+    if (obs_dim == 14) run(std::integral_constant<int, 14>{}, std::integral_constant<int, 3>{});
+    else run(std::integral_constant<int, 7>{}, std::integral_constant<int, 2>{});
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_ppo_grad: launch");
 }
 
 

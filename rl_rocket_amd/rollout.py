@@ -439,8 +439,88 @@ def _allreduce_grads(params, group):
         k += g.numel()
 
 
+def _policy_tensors(policy):
+    """The 13 parameter tensors in rr_policy_pack / rr_ppo_grad order."""
+    p = policy
+    return [p.pi_net[0].weight, p.pi_net[0].bias, p.pi_net[2].weight, p.pi_net[2].bias,
+            p.vf_net[0].weight, p.vf_net[0].bias, p.vf_net[2].weight, p.vf_net[2].bias,
+            p.action_net.weight, p.action_net.bias, p.value_net.weight, p.value_net.bias, p.log_std]
+
+
+def fused_grad_supported(policy, obs_dim, act_dim):
+    return (isinstance(policy, MlpActorCritic) and policy.hidden == (64, 64)
+            and (obs_dim, act_dim) in ((14, 3), (7, 2)))
+
+
+class PPOGrad:
+    """The PPO minibatch loss + backward as ONE HIP pipeline (``rr_ppo_grad``: fp32 MFMA forward
+    and backward of both towers over the gathered minibatch, fixed-order workgroup sums).
+
+    ``__call__(idx)`` WRITES ``p.grad`` of the policy's 13 parameters (allocated here once and
+    kept: the library holds their addresses, so do not set them to None — use
+    ``zero_grad(set_to_none=False)`` or none at all, the call overwrites) for the minibatch
+    ``idx`` (int64 device tensor of 2 .. ``batch_size`` rows of the flattened rollout) and fills
+    ``stats`` = [policy_loss, value_loss, entropy, clip_fraction, approx_kl]. Same loss as
+    ``ppo_update`` (SB3 1.6 PPO.train); gradients equal autograd's to fp32 rounding
+    (``tests/test_gpu_ppo.py``). Stream-ordered on the current stream; graph-capturable."""
+
+    def __init__(self, policy, ro, batch_size, clip_range=0.2, ent_coef=0.01, vf_coef=0.5):
+        import ctypes
+
+        from . import _lib
+
+        n = ro.n_steps * ro.env.num_envs
+        ns, na = ro.env.state_dim, ro.env.action_dim
+        if not fused_grad_supported(policy, ns, na):
+            raise ValueError("PPOGrad needs an MlpActorCritic with 64x64 towers and (obs, act) in ((14, 3), (7, 2))")
+        if not 2 <= batch_size <= n:
+            raise ValueError("batch_size must be in [2, n_steps * num_envs]")
+        self._lib, self._c = _lib.load(), ctypes
+        self.ns, self.na, self.bs = ns, na, int(batch_size)
+        self.coef = (float(clip_range), float(ent_coef), float(vf_coef))
+        dev = ro.obs.device
+        self.data = [ro.obs.reshape(n, ns), ro.actions.reshape(n, na), ro.log_probs.reshape(n),
+                     ro.advantages.reshape(n), ro.returns.reshape(n)]
+        for t in self.data:
+            if not t.is_contiguous() or t.dtype != torch.float32:
+                raise ValueError("rollout tensors must be contiguous fp32")
+        self.params = _policy_tensors(policy)
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous() or p.device != dev:
+                raise ValueError("rr_ppo_grad needs contiguous fp32 parameters on the rollout device")
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        nbytes = ctypes.c_int64()
+        _lib.check(self._lib.rr_ppo_workspace_size(ns, na, self.bs, ctypes.byref(nbytes)), "rr_ppo_workspace_size")
+        self.ws = torch.empty((nbytes.value + 15) // 16 * 4, dtype=torch.float32, device=dev)
+        self.stats = torch.zeros(5, dtype=torch.float32, device=dev)
+        self._src = (ctypes.c_void_p * 13)(*[p.data_ptr() for p in self.params])
+        self._grads = [p.grad for p in self.params]
+        self._dst = (ctypes.c_void_p * 13)(*[g.data_ptr() for g in self._grads])
+        self._nbytes = nbytes.value
+
+    def __call__(self, idx):
+        from . import _lib
+
+        c = self._c
+        if (idx.dtype != torch.int64 or not 2 <= idx.numel() <= self.bs or not idx.is_contiguous()
+                or idx.device != self.ws.device):
+            raise ValueError("idx must be a contiguous int64 device tensor of 2 .. batch_size rows")
+        for p, g in zip(self.params, self._grads):
+            if p.grad is not g:
+                raise RuntimeError("a parameter's .grad was replaced; PPOGrad writes into the tensors it allocated")
+        clip, ent, vf = self.coef
+        o, a, lp, adv, ret = self.data
+        stream = c.c_void_p(torch.cuda.current_stream(self.ws.device).cuda_stream)
+        _lib.check(self._lib.rr_ppo_grad(self.ns, self.na, self._src, self._dst, o.data_ptr(), a.data_ptr(),
+                                         lp.data_ptr(), adv.data_ptr(), ret.data_ptr(), idx.data_ptr(), idx.numel(),
+                                         clip, ent, vf, self.stats.data_ptr(), self.ws.data_ptr(), self._nbytes,
+                                         stream), "rr_ppo_grad")
+        return self.stats
+
+
 def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=0.2, ent_coef=0.01,
-               vf_coef=0.5, max_grad_norm=0.5, generator=None, group=None):
+               vf_coef=0.5, max_grad_norm=0.5, generator=None, group=None, fused=False):
     """SB3 1.6 PPO.train on the device-resident rollout (advantage normalisation per
     minibatch, clipped surrogate, unclipped value loss, entropy bonus, grad-norm clip).
     ent_coef 0.01 as main_6DOF.py:68.
@@ -450,8 +530,24 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
     minibatch gradients are averaged over the ranks (one all_reduce) before the grad-norm
     clip and the optimizer step, so replicas that start equal stay equal. Ranks must run
     the same number of minibatches (equal shard sizes); advantages are normalised per
-    rank's minibatch."""
+    rank's minibatch.
+
+    ``fused=True``: the loss + backward of every minibatch is ``PPOGrad`` (one HIP pipeline)
+    instead of PyTorch autograd; the optimizer, the clip and the all_reduce are unchanged."""
     n = ro.n_steps * ro.env.num_envs
+    if fused:
+        grad = PPOGrad(policy, ro, min(batch_size, n), clip_range, ent_coef, vf_coef)
+        params = list(policy.parameters())
+        stats = None
+        for _ in range(n_epochs):
+            perm = torch.randperm(n, device=ro.obs.device, generator=generator)
+            for s in range(0, n, grad.bs):
+                stats = grad(perm[s:s + grad.bs])
+                if group is not None:
+                    _allreduce_grads(params, group)
+                torch.nn.utils.clip_grad_norm_(params, max_grad_norm)
+                optimizer.step()
+        return {} if stats is None else dict(zip(("policy_loss", "value_loss", "entropy"), stats[:3].tolist()))
     obs = ro.obs.reshape(n, -1)
     act = ro.actions.reshape(n, -1)
     old_lp = ro.log_probs.reshape(n)
@@ -484,20 +580,25 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
 class GraphedPPOUpdate:
     """``ppo_update``'s minibatch step — gather, forward, clipped-surrogate / value / entropy
     loss, backward, (multi-GPU gradient all_reduce), grad-norm clip, Adam step — captured ONCE
-    into a hipGraph and replayed per minibatch: the ~80 small launches and their Python driving
-    become one graph launch (the update of configs[4] is otherwise host-bound: a 64x64 MLP on
-    65 536 samples is a few microseconds of device work per kernel).
+    into a hipGraph and replayed per minibatch.
+
+    ``fused`` (default: wherever ``PPOGrad`` supports the policy) takes the loss + backward from
+    ``PPOGrad`` (rr_ppo_grad: one fp32-MFMA HIP pipeline) instead of PyTorch autograd, whose
+    tall-skinny GEMMs over the 65 536-row minibatch run far below the GPU's rate (the weight
+    gradient dW = g^T x alone ~190 us per layer: tools/probe_bias_grad.py); the gradients then
+    match the eager update's to fp32 rounding instead of bitwise. ``fused=False`` captures the
+    PyTorch ops themselves (bitwise the eager ``ppo_update``).
 
     Needs an optimizer created with ``capturable=True`` (``torch.optim.Adam(..., capturable=True)``:
     its step count lives on the device) and ``n_steps * num_envs`` divisible by ``batch_size``.
     The warm-up steps the capture requires run on the real parameters and are undone (parameters
     and optimizer state restored in place), so the first ``update`` starts from the same state
-    as the eager ``ppo_update`` would, and computes the same minibatch steps (same kernels, same
-    order; ``tests/test_gpu_rollout.py``). Multi-GPU: ``group`` must be an RCCL ("nccl") group —
+    as the eager ``ppo_update`` would, and computes the same minibatch steps (``fused=False``: same
+    kernels, same order; ``tests/test_gpu_rollout.py``). Multi-GPU: ``group`` must be an RCCL ("nccl") group —
     the all_reduce is captured with the rest."""
 
     def __init__(self, policy, optimizer, ro, batch_size=65536, clip_range=0.2, ent_coef=0.01, vf_coef=0.5,
-                 max_grad_norm=0.5, group=None):
+                 max_grad_norm=0.5, group=None, fused=None):
         if not all(g.get("capturable", False) for g in optimizer.param_groups):
             raise ValueError("GraphedPPOUpdate needs an optimizer with capturable=True")
         n = ro.n_steps * ro.env.num_envs
@@ -530,6 +631,10 @@ class GraphedPPOUpdate:
         self.params = params
         for p in params:
             p.grad = torch.zeros_like(p)
+        if fused is None:
+            fused = fused_grad_supported(policy, ro.env.state_dim, ro.env.action_dim)
+        self.fused = bool(fused)
+        self._grad = PPOGrad(policy, ro, batch_size, clip_range, ent_coef, vf_coef) if self.fused else None
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
@@ -558,6 +663,13 @@ class GraphedPPOUpdate:
     def _step(self):
         clip_range, ent_coef, vf_coef, max_grad_norm = self.coef
         pol, i = self.policy, self.idx
+        if self.fused:
+            st = self._grad(i)
+            if self.group is not None:
+                _allreduce_grads(self.params, self.group)
+            torch.nn.utils.clip_grad_norm_(self.params, max_grad_norm)
+            self.optimizer.step()
+            return {"policy_loss": st[0], "value_loss": st[1], "entropy": st[2]}
         mean, value = pol(self.obs[i])
         lp = pol.log_prob(mean, self.act[i])
         adv = self.adv_all[i]

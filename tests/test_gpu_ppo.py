@@ -1,0 +1,171 @@
+"""rr_ppo_grad (rl_rocket_amd/csrc/rocket_ppo.inc, PPOGrad): the PPO minibatch loss + backward of
+the MlpPolicy on fp32 MFMA, against PyTorch autograd of the same loss (rollout.ppo_update's,
+SB3 1.6 PPO.train) evaluated in float64 on the same parameters and minibatch.
+
+Tolerance: per gradient tensor, max |fused - fp64| <= 1e-4 * max |fp64| + 1e-7 (fp32 sums over
+up to 65 536 samples in another order, tanh via exp2 / rcp: the PyTorch fp32 autograd of the same
+loss lands at the same level, printed beside it). Stats (policy_loss, value_loss, entropy,
+clip_fraction, approx_kl) within 1e-5 relative + 1e-6 (clip_fraction: within 2 samples)."""
+import copy
+import types
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(ns, na, n, seed=0):
+    import torch
+    from rl_rocket_amd.rollout import MlpActorCritic
+
+    g = torch.Generator("cuda:0").manual_seed(seed)
+    torch.manual_seed(seed)
+    pol = MlpActorCritic(ns, na).cuda()
+    with torch.no_grad():  # off SB3's small-gain init so every weight and bias matters
+        for p in pol.parameters():
+            p.add_(0.2 * torch.randn(p.shape, device="cuda:0", generator=g))
+    f = dict(device="cuda:0", dtype=torch.float32)
+    obs = 0.7 * torch.randn((n, ns), generator=g, **f)
+    act = torch.randn((n, na), generator=g, **f)
+    with torch.no_grad():
+        mean, _ = pol(obs)
+        old_lp = pol.log_prob(mean, act) + 0.25 * torch.randn((n,), generator=g, **f)  # ratios on both sides of the clip
+    adv = 2.0 * torch.randn((n,), generator=g, **f) + 0.3
+    ret = 5.0 * torch.randn((n,), generator=g, **f)
+    ro = types.SimpleNamespace(n_steps=1, env=types.SimpleNamespace(num_envs=n, state_dim=ns, action_dim=na),
+                               obs=obs.view(1, n, ns), actions=act.view(1, n, na), log_probs=old_lp.view(1, n),
+                               advantages=adv.view(1, n), returns=ret.view(1, n))
+    return pol, ro, g
+
+
+def _reference(pol, ro, idx, dtype, clip=0.2, ent_coef=0.01, vf_coef=0.5):
+    """ppo_update's loss for one minibatch (autograd) in `dtype`."""
+    import torch
+    from rl_rocket_amd.rollout import _policy_tensors
+
+    p = copy.deepcopy(pol).to(dtype)
+    n = ro.env.num_envs
+    obs = ro.obs.reshape(n, -1)[idx].to(dtype)
+    act = ro.actions.reshape(n, -1)[idx].to(dtype)
+    old = ro.log_probs.reshape(n)[idx].to(dtype)
+    adv = ro.advantages.reshape(n)[idx].to(dtype)
+    ret = ro.returns.reshape(n)[idx].to(dtype)
+    mean, value = p(obs)
+    lp = p.log_prob(mean, act)
+    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    ratio = torch.exp(lp - old)
+    pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+    vf = torch.nn.functional.mse_loss(ret, value)
+    ent = -p.entropy(len(idx)).mean()
+    (pg + ent_coef * ent + vf_coef * vf).backward()
+    with torch.no_grad():
+        lr = lp - old
+        stats = [pg.item(), vf.item(), -ent.item(), ((ratio - 1).abs() > clip).double().mean().item(),
+                 ((torch.exp(lr) - 1) - lr).mean().item()]
+    return [t.grad.double() for t in _policy_tensors(p)], stats
+
+
+NAMES = ["pi.W1", "pi.b1", "pi.W2", "pi.b2", "vf.W1", "vf.b1", "vf.W2", "vf.b2", "W_action", "b_action",
+         "W_value", "b_value", "log_std"]
+
+
+@pytest.mark.parametrize("ns,na", [(14, 3), (7, 2)])
+@pytest.mark.parametrize("bs", [65536, 1000, 2])
+def test_ppo_grad_matches_autograd(ns, na, bs):
+    import torch
+    from rl_rocket_amd.rollout import PPOGrad, _policy_tensors
+
+    n = 70000
+    pol, ro, g = _setup(ns, na, n, seed=ns + bs)
+    idx = torch.randperm(n, device="cuda:0", generator=g)[:bs].contiguous()
+    grad = PPOGrad(pol, ro, bs)
+    stats = grad(idx).tolist()
+    torch.cuda.synchronize()
+    fused = [t.grad.double() for t in _policy_tensors(pol)]
+    ref64, st64 = _reference(pol, ro, idx, torch.float64)
+    ref32, _ = _reference(pol, ro, idx, torch.float32)
+    for name, a, r, t in zip(NAMES, fused, ref64, ref32):
+        scale = r.abs().max().item()
+        err, err32 = (a - r).abs().max().item(), (t - r).abs().max().item()
+        print("%-9s max|ref| %.3e  fused err %.2e  torch-fp32 err %.2e" % (name, scale, err, err32))
+        assert err <= 1e-4 * scale + 1e-7, (name, err, scale, err32)
+    for k, (a, r) in enumerate(zip(stats, st64)):
+        tol = 2.0 / bs if k == 3 else 1e-5 * abs(r) + 1e-6
+        assert abs(a - r) <= tol, (k, a, r)
+
+
+def test_ppo_grad_overwrites_and_is_deterministic():
+    """Two calls on the same minibatch give bitwise the same gradients (fixed-order sums), written
+    over whatever the .grad tensors held."""
+    import torch
+    from rl_rocket_amd.rollout import PPOGrad, _policy_tensors
+
+    n = 20000
+    pol, ro, g = _setup(14, 3, n, seed=3)
+    idx = torch.randperm(n, device="cuda:0", generator=g)[:8192].contiguous()
+    grad = PPOGrad(pol, ro, 8192)
+    grad(idx)
+    first = [t.grad.clone() for t in _policy_tensors(pol)]
+    for t in _policy_tensors(pol):
+        t.grad.fill_(123.0)
+    grad(idx)
+    for a, t in zip(first, _policy_tensors(pol)):
+        assert torch.equal(a, t.grad)
+
+
+def test_fused_update_graphed_equals_eager_and_tracks_autograd():
+    """ppo_update(fused=True) and GraphedPPOUpdate(fused=True) from the same state and shuffling:
+    bitwise equal (same launches in the same order); and against the PyTorch-autograd ppo_update,
+    with Adam(eps=1.0) so that parameter steps are proportional to the gradients (not their
+    signs): within 1e-6 after two epochs."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout, GraphedPPOUpdate, MlpActorCritic, ppo_update
+
+    n, T, bs = 8192, 8, 16384
+    env = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=30, **ENV_CONFIG_6DOF)
+    torch.manual_seed(11)
+    pol = MlpActorCritic(14, 3).cuda()
+    ro = DeviceRollout(env, pol, n_steps=T, seed=4)
+    ro.collect()
+    torch.cuda.synchronize()
+    pols = [copy.deepcopy(pol) for _ in range(3)]
+    opts = [torch.optim.Adam(p.parameters(), lr=1e-3, eps=1.0, capturable=True) for p in pols]
+    g = GraphedPPOUpdate(pols[2], opts[2], ro, batch_size=bs, fused=True)
+    assert g.fused
+    gen = lambda: torch.Generator("cuda:0").manual_seed(9)  # noqa: E731
+    sa = ppo_update(pols[0], opts[0], ro, n_epochs=2, batch_size=bs, generator=gen())
+    sb = ppo_update(pols[1], opts[1], ro, n_epochs=2, batch_size=bs, generator=gen(), fused=True)
+    sc = g.update(n_epochs=2, generator=gen())
+    torch.cuda.synchronize()
+    for x, y in zip(pols[1].parameters(), pols[2].parameters()):
+        assert torch.equal(x, y)
+    moved = max((x - y).abs().max().item() for x, y in zip(pol.parameters(), pols[1].parameters()))
+    worst = max((x - y).abs().max().item() for x, y in zip(pols[0].parameters(), pols[1].parameters()))
+    print("moved %.3e, fused vs autograd %.3e" % (moved, worst))
+    assert moved > 1e-5
+    assert worst <= 1e-6, worst
+    for k in sa:
+        assert abs(sa[k] - sb[k]) <= 1e-4 * max(1.0, abs(sa[k])), (k, sa[k], sb[k])
+        assert abs(sb[k] - sc[k]) <= 1e-6 * max(1.0, abs(sb[k])), (k, sb[k], sc[k])
+    env.close()
+
+
+def test_ppo_grad_rejects_bad_arguments():
+    import torch
+    from rl_rocket_amd.rollout import PPOGrad
+
+    pol, ro, g = _setup(14, 3, 1000, seed=1)
+    grad = PPOGrad(pol, ro, 512)
+    with pytest.raises(ValueError):
+        grad(torch.arange(513, device="cuda:0"))  # more rows than the workspace was sized for
+    with pytest.raises(ValueError):
+        grad(torch.arange(1, device="cuda:0"))  # a 1-sample minibatch has no std
+    with pytest.raises(ValueError):
+        grad(torch.arange(512, device="cuda:0", dtype=torch.int32))
+    pol.pi_net[0].bias.grad = None
+    with pytest.raises(RuntimeError):
+        grad(torch.arange(512, device="cuda:0"))
+    with pytest.raises(ValueError):
+        PPOGrad(pol, ro, 1)

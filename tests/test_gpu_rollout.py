@@ -377,7 +377,7 @@ def test_graphed_ppo_update_equals_eager():
     pa, pb = copy.deepcopy(pol), copy.deepcopy(pol)
     oa = torch.optim.Adam(pa.parameters(), lr=3e-4, eps=1e-5, capturable=True)
     ob = torch.optim.Adam(pb.parameters(), lr=3e-4, eps=1e-5, capturable=True)
-    g = GraphedPPOUpdate(pb, ob, ro, batch_size=bs)
+    g = GraphedPPOUpdate(pb, ob, ro, batch_size=bs, fused=False)
     for x, y in zip(pa.parameters(), pb.parameters()):  # warm-up undone
         assert torch.equal(x, y)
     sa = ppo_update(pa, oa, ro, n_epochs=2, batch_size=bs, generator=torch.Generator("cuda:0").manual_seed(5))

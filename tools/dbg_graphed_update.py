@@ -15,7 +15,7 @@ oa = torch.optim.Adam(pa.parameters(), lr=3e-4, eps=1e-5, capturable=True)
 ob = torch.optim.Adam(pb.parameters(), lr=3e-4, eps=1e-5, capturable=True)
 oc = torch.optim.Adam(pc.parameters(), lr=3e-4, eps=1e-5, capturable=True)
 MG = float(os.environ.get("MG", "0.5"))
-g = GraphedPPOUpdate(pb, ob, ro, batch_size=bs, max_grad_norm=MG)
+g = GraphedPPOUpdate(pb, ob, ro, batch_size=bs, max_grad_norm=MG, fused=False)
 # eager, with the graph object's own _step on a third copy through an eager GraphedPPOUpdate-like loop
 perm = torch.randperm(n * T, device="cuda:0", generator=torch.Generator("cuda:0").manual_seed(5))
 for s in range(0, n * T, bs):
