@@ -317,13 +317,28 @@ int rr_gae(int64_t T, int64_t n, const float* rewards, const float* values, cons
  * accumulated). stats (device, 5 floats, or NULL): policy_loss, value_loss, entropy,
  * clip_fraction, approx_kl (SB3's logged quantities). Deterministic (fixed-order sums, no
  * atomics); fp32 MFMA, so the gradients equal PyTorch's autograd ones to fp32 summation-order
- * rounding. Four launches on `stream`, capturable in a graph. Supported (obs_dim, act_dim):
+ * rounding. Three launches on `stream`, capturable in a graph. Supported (obs_dim, act_dim):
  * (14, 3), (7, 2); batch >= 2. workspace: device, 16-B aligned, rr_ppo_workspace_size bytes. */
 int rr_ppo_workspace_size(int obs_dim, int act_dim, int64_t batch, int64_t* bytes);
 int rr_ppo_grad(int obs_dim, int act_dim, const float* const* params, float* const* grads, const float* obs,
                 const float* actions, const float* old_log_prob, const float* advantages, const float* returns,
                 const int64_t* idx, int64_t batch, float clip_range, float ent_coef, float vf_coef, float* stats,
                 void* workspace, int64_t workspace_bytes, void* stream);
+
+/* torch.nn.utils.clip_grad_norm_(max_grad_norm) + one torch.optim.Adam(capturable=True) step
+ * (weight_decay 0, no amsgrad / maximize) over n_tensors (<= 16) fp32 device tensors, in two
+ * launches: the rest of SB3 PPO.train's minibatch step after rr_ppo_grad. grads are scaled in
+ * place by min(1, max_grad_norm / (||grads|| + 1e-6)) (no clip when max_grad_norm <= 0);
+ * exp_avg / exp_avg_sq / step are the optimizer's state tensors (optimizer.state[p]: "exp_avg",
+ * "exp_avg_sq", and the device float "step", incremented), updated in place with PyTorch's
+ * capturable multi-tensor formulas; lr is a DEVICE float, read at run time (a learning-rate
+ * schedule can change it between graph replays). Arrays are host arrays of device pointers;
+ * numel[] host. workspace: device, rr_clip_adam_workspace_size(sum of numel) bytes. */
+int rr_clip_adam_workspace_size(int64_t total_elements, int64_t* bytes);
+int rr_clip_adam(int n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
+                 float* const* exp_avg_sq, float* const* step, const int64_t* numel, float max_grad_norm,
+                 const float* lr, double beta1, double beta2, float eps, void* workspace, int64_t workspace_bytes,
+                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -118,6 +118,9 @@ SIGNATURES = {
                                           ctypes.c_float] + [_P] * 17),
     "rr_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, _P,
                               _P, _P]),
+    "rr_clip_adam_workspace_size": (ctypes.c_int, [ctypes.c_int64, _P]),
+    "rr_clip_adam": (ctypes.c_int, [ctypes.c_int, _P, _P, _P, _P, _P, _P, ctypes.c_float, _P, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_float, _P, ctypes.c_int64, _P]),
     "rr_ppo_workspace_size": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int64, _P]),
     "rr_ppo_grad": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_int64,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, ctypes.c_int64, _P]),

@@ -2240,14 +2240,61 @@ int64_t ppo_part_floats(int obs_dim, int act_dim)
     if (obs_dim == 7 && act_dim == 2) return ppo::Part<7, 2>::SIZE;
     return 0;
 }
+
+int64_t ppo_pack_floats(int obs_dim, int act_dim)
+{
+    return obs_dim == 14 ? ppo::Pack<14, 3>::SIZE : ppo::Pack<7, 2>::SIZE;
+}
 }  // namespace
+
+int rr_clip_adam_workspace_size(int64_t total_elements, int64_t* bytes)
+{
+    if (total_elements < 1 || !bytes) return fail(RR_EINVAL, "rr_clip_adam_workspace_size: total_elements >= 1");
+    *bytes = ((total_elements + kAdamThreads - 1) / kAdamThreads + 1) * (int64_t)sizeof(float);
+    return RR_OK;
+}
+
+int rr_clip_adam(int n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
+                 float* const* exp_avg_sq, float* const* step, const int64_t* numel, float max_grad_norm,
+                 const float* lr, double beta1, double beta2, float eps, void* workspace, int64_t workspace_bytes,
+                 void* stream)
+{
+    if (n_tensors < 1 || n_tensors > 16) return fail(RR_EINVAL, "rr_clip_adam: 1 .. 16 tensors");
+    if (!params || !grads || !exp_avg || !exp_avg_sq || !step || !numel || !lr || !workspace)
+        return fail(RR_EINVAL, "rr_clip_adam: null argument");
+    AdamList a = {};
+    a.n = n_tensors;
+    for (int t = 0; t < n_tensors; ++t) {
+        if (!params[t] || !grads[t] || !exp_avg[t] || !exp_avg_sq[t] || !step[t] || numel[t] < 1)
+            return fail(RR_EINVAL, "rr_clip_adam: null or empty tensor");
+        a.param[t] = params[t];
+        a.grad[t] = grads[t];
+        a.exp_avg[t] = exp_avg[t];
+        a.exp_avg_sq[t] = exp_avg_sq[t];
+        a.step[t] = step[t];
+        a.start[t + 1] = a.start[t] + numel[t];
+    }
+    int64_t need = 0;
+    rr_clip_adam_workspace_size(a.start[n_tensors], &need);
+    if (workspace_bytes < need) return fail(RR_EINVAL, "rr_clip_adam: workspace smaller than rr_clip_adam_workspace_size");
+    const dim3 grid((unsigned)((a.start[n_tensors] + kAdamThreads - 1) / kAdamThreads));
+    hipStream_t s = (hipStream_t)stream;
+    float* work = (float*)workspace;
+    hipLaunchKernelGGL(adam_norm_kernel, grid, dim3(kAdamThreads), 0, s, a, work);
+    hipLaunchKernelGGL(adam_step_kernel, grid, dim3(kAdamThreads), 0, s, a, work, max_grad_norm, lr, (float)beta1,
+                       (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps);
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_clip_adam: launch");
+}
 
 int rr_ppo_workspace_size(int obs_dim, int act_dim, int64_t batch, int64_t* bytes)
 {
     const int64_t pf = ppo_part_floats(obs_dim, act_dim);
     if (!pf) return fail(RR_EINVAL, "rr_ppo_workspace_size: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
     if (batch < 2 || !bytes) return fail(RR_EINVAL, "rr_ppo_workspace_size: batch >= 2 and bytes required");
-    *bytes = (int64_t)(2 * ppo::kAdvPart * sizeof(double)) + 2 * ppo_nwg(batch) * pf * (int64_t)sizeof(float);
+    // adv partial sums | 2 towers x nwg partial-gradient vectors | 2 packed tower images
+    *bytes = (int64_t)(2 * ppo::kAdvPart * sizeof(double)) +
+             2 * (ppo_nwg(batch) * pf + ppo_pack_floats(obs_dim, act_dim)) * (int64_t)sizeof(float);
     return RR_OK;
 }
 
@@ -2275,13 +2322,16 @@ int rr_ppo_grad(int obs_dim, int act_dim, const float* const* params, float* con
     double* adv_part = (double*)workspace;
     float* part = (float*)((char*)workspace + 2 * ppo::kAdvPart * sizeof(double));
     const int nwg = (int)ppo_nwg(batch);
-    hipLaunchKernelGGL(ppo_adv_kernel, dim3(ppo::kAdvPart), dim3(256), 0, s, advantages, idx, batch, adv_part);
     auto run = [&](auto obs_c, auto act_c) {
         constexpr int O = decltype(obs_c)::value, A = decltype(act_c)::value;
         using PT = ppo::Part<O, A>;
-        hipLaunchKernelGGL((ppo_grad_kernel<O, A>), dim3(nwg, 2), dim3(ppo::kThreads), 0, s, ps, obs, actions,
-                           old_log_prob, advantages, returns, idx, batch, clip_range, vf_coef, adv_part, part);
-        hipLaunchKernelGGL((ppo_finish_kernel<O, A>), dim3((PT::SIZE + 63) / 64, 2), dim3(256), 0, s, part, nwg, batch,
+        using K = ppo::Pack<O, A>;
+        float* pack = part + 2 * (int64_t)nwg * PT::SIZE;  // 16-B aligned: PT::SIZE % 4 == 0
+        hipLaunchKernelGGL((ppo_prep_kernel<O, A>), dim3(ppo::kAdvPart + (2 * K::SIZE + 255) / 256), dim3(256), 0, s,
+                           advantages, idx, batch, adv_part, ps, pack);
+        hipLaunchKernelGGL((ppo_grad_kernel<O, A>), dim3(nwg, 2), dim3(ppo::kThreads), 0, s, obs, actions,
+                           old_log_prob, advantages, returns, idx, batch, clip_range, vf_coef, adv_part, pack, part);
+        hipLaunchKernelGGL((ppo_finish_kernel<O, A>), dim3((PT::SIZE + kFinElems - 1) / kFinElems, 2), dim3(256), 0, s, part, nwg, batch,
                            ent_coef, ps, pg, stats);
     };
     if (obs_dim == 14) run(std::integral_constant<int, 14>{}, std::integral_constant<int, 3>{});

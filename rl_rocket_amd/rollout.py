@@ -519,6 +519,82 @@ class PPOGrad:
         return self.stats
 
 
+def clip_adam_supported(optimizer, params):
+    if type(optimizer) is not torch.optim.Adam or len(optimizer.param_groups) != 1:
+        return False
+    g = optimizer.param_groups[0]
+    if {id(p) for p in g["params"]} != {id(p) for p in params} or len(params) > 16:
+        return False
+    return (g.get("capturable", False) and not g.get("amsgrad", False) and not g.get("maximize", False)
+            and g.get("weight_decay", 0) == 0 and not torch.is_tensor(g["betas"][0])
+            and all(p.dtype == torch.float32 and p.is_contiguous() and p.is_cuda for p in params))
+
+
+class ClipAdam:
+    """``clip_grad_norm_(params, max_grad_norm)`` + ``optimizer.step()`` for a
+    ``torch.optim.Adam(capturable=True)`` in two launches (``rr_clip_adam``), on the optimizer's own
+    state tensors (created here, as Adam's first step would, if absent), so the optimizer object
+    stays the source of truth (state_dict, later eager steps). The learning rate is read from a
+    device scalar that ``__call__`` refreshes from ``param_groups[0]["lr"]`` when called eagerly;
+    inside a captured graph call ``sync_lr()`` before replays (GraphedPPOUpdate.update does)."""
+
+    def __init__(self, optimizer, params, max_grad_norm):
+        import ctypes
+
+        from . import _lib
+
+        if not clip_adam_supported(optimizer, params):
+            raise ValueError("ClipAdam needs a capturable torch.optim.Adam over exactly these fp32 CUDA parameters "
+                             "(one group, no weight decay / amsgrad / maximize, <= 16 tensors)")
+        self.opt, self.params = optimizer, list(params)
+        self.max_norm = float(max_grad_norm) if max_grad_norm is not None else 0.0
+        dev = self.params[0].device
+        for p in self.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            st = optimizer.state[p]
+            if not st:
+                st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            if not st["step"].is_cuda or st["step"].dtype != torch.float32:
+                raise ValueError("ClipAdam needs the capturable Adam's device float32 step tensors")
+        self.lr = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.sync_lr()
+        n = len(self.params)
+        P = ctypes.c_void_p * n
+        self._tensors = [(p, p.grad, optimizer.state[p]["exp_avg"], optimizer.state[p]["exp_avg_sq"],
+                          optimizer.state[p]["step"]) for p in self.params]
+        self._ptrs = [P(*[t[k].data_ptr() for t in self._tensors]) for k in range(5)]
+        self._numel = (ctypes.c_int64 * n)(*[p.numel() for p in self.params])
+        self._lib, self._c = _lib.load(), ctypes
+        nbytes = ctypes.c_int64()
+        _lib.check(self._lib.rr_clip_adam_workspace_size(sum(p.numel() for p in self.params), ctypes.byref(nbytes)),
+                   "rr_clip_adam_workspace_size")
+        self._ws = torch.empty((nbytes.value + 3) // 4, dtype=torch.float32, device=dev)
+        self._nbytes = nbytes.value
+
+    def sync_lr(self):
+        self.lr.fill_(float(self.opt.param_groups[0]["lr"]))
+
+    def __call__(self):
+        from . import _lib
+
+        for p, g, m, v, s in self._tensors:
+            st = self.opt.state[p]
+            if p.grad is not g or st["exp_avg"] is not m or st["exp_avg_sq"] is not v or st["step"] is not s:
+                raise RuntimeError("a gradient or Adam state tensor was replaced; ClipAdam holds their addresses")
+        if not torch.cuda.is_current_stream_capturing():
+            self.sync_lr()
+        grp = self.opt.param_groups[0]
+        b1, b2 = grp["betas"]
+        _lib.check(self._lib.rr_clip_adam(len(self.params), *self._ptrs, self._numel, self.max_norm,
+                                          self.lr.data_ptr(), float(b1), float(b2), float(grp["eps"]),
+                                          self._ws.data_ptr(), self._nbytes,
+                                          self._c.c_void_p(torch.cuda.current_stream(self.lr.device).cuda_stream)),
+                   "rr_clip_adam")
+
+
 def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=0.2, ent_coef=0.01,
                vf_coef=0.5, max_grad_norm=0.5, generator=None, group=None, fused=False):
     """SB3 1.6 PPO.train on the device-resident rollout (advantage normalisation per
@@ -533,11 +609,13 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
     rank's minibatch.
 
     ``fused=True``: the loss + backward of every minibatch is ``PPOGrad`` (one HIP pipeline)
-    instead of PyTorch autograd; the optimizer, the clip and the all_reduce are unchanged."""
+    instead of PyTorch autograd, and for a capturable Adam the clip + optimizer step is
+    ``ClipAdam`` (one launch) on the optimizer's own state; the all_reduce is unchanged."""
     n = ro.n_steps * ro.env.num_envs
     if fused:
         grad = PPOGrad(policy, ro, min(batch_size, n), clip_range, ent_coef, vf_coef)
         params = list(policy.parameters())
+        adam = ClipAdam(optimizer, params, max_grad_norm) if clip_adam_supported(optimizer, params) else None
         stats = None
         for _ in range(n_epochs):
             perm = torch.randperm(n, device=ro.obs.device, generator=generator)
@@ -545,8 +623,11 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
                 stats = grad(perm[s:s + grad.bs])
                 if group is not None:
                     _allreduce_grads(params, group)
-                torch.nn.utils.clip_grad_norm_(params, max_grad_norm)
-                optimizer.step()
+                if adam is not None:
+                    adam()
+                else:
+                    torch.nn.utils.clip_grad_norm_(params, max_grad_norm)
+                    optimizer.step()
         return {} if stats is None else dict(zip(("policy_loss", "value_loss", "entropy"), stats[:3].tolist()))
     obs = ro.obs.reshape(n, -1)
     act = ro.actions.reshape(n, -1)
@@ -635,6 +716,8 @@ class GraphedPPOUpdate:
             fused = fused_grad_supported(policy, ro.env.state_dim, ro.env.action_dim)
         self.fused = bool(fused)
         self._grad = PPOGrad(policy, ro, batch_size, clip_range, ent_coef, vf_coef) if self.fused else None
+        self._adam = (ClipAdam(optimizer, params, max_grad_norm)
+                      if self.fused and clip_adam_supported(optimizer, params) else None)
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
@@ -667,8 +750,11 @@ class GraphedPPOUpdate:
             st = self._grad(i)
             if self.group is not None:
                 _allreduce_grads(self.params, self.group)
-            torch.nn.utils.clip_grad_norm_(self.params, max_grad_norm)
-            self.optimizer.step()
+            if self._adam is not None:
+                self._adam()
+            else:
+                torch.nn.utils.clip_grad_norm_(self.params, max_grad_norm)
+                self.optimizer.step()
             return {"policy_loss": st[0], "value_loss": st[1], "entropy": st[2]}
         mean, value = pol(self.obs[i])
         lp = pol.log_prob(mean, self.act[i])
@@ -690,6 +776,8 @@ class GraphedPPOUpdate:
     def update(self, n_epochs=10, generator=None):
         """n_epochs passes over the rollout in shuffled minibatches (ppo_update's order:
         one torch.randperm per epoch)."""
+        if self._adam is not None:
+            self._adam.sync_lr()  # the graph reads lr from the device: follow param_groups[0]["lr"]
         for _ in range(n_epochs):
             perm = torch.randperm(self.n, device=self.obs.device, generator=generator)
             for s in range(0, self.n, self.bs):

@@ -169,3 +169,40 @@ def test_ppo_grad_rejects_bad_arguments():
         grad(torch.arange(512, device="cuda:0"))
     with pytest.raises(ValueError):
         PPOGrad(pol, ro, 1)
+
+
+def test_clip_adam_matches_torch():
+    """rr_clip_adam (ClipAdam) against clip_grad_norm_ + torch.optim.Adam(capturable=True) on the
+    same gradients for 6 steps (clip active on the first 3, a learning-rate change after 3):
+    parameters, clipped gradients and the optimizer's exp_avg / exp_avg_sq / step within fp32
+    rounding."""
+    import torch
+    from rl_rocket_amd.rollout import ClipAdam, MlpActorCritic
+
+    torch.manual_seed(5)
+    pa = MlpActorCritic(14, 3).cuda()
+    pb = copy.deepcopy(pa)
+    oa = torch.optim.Adam(pa.parameters(), lr=3e-4, eps=1e-5, capturable=True)
+    ob = torch.optim.Adam(pb.parameters(), lr=3e-4, eps=1e-5, capturable=True)
+    adam = ClipAdam(ob, list(pb.parameters()), 0.5)
+    g = torch.Generator("cuda:0").manual_seed(2)
+    for step in range(6):
+        if step == 3:
+            for o in (oa, ob):
+                o.param_groups[0]["lr"] = 1e-4
+        scale = 1.0 if step < 3 else 1e-3
+        for x, y in zip(pa.parameters(), pb.parameters()):
+            gr = scale * torch.randn(x.shape, device="cuda:0", generator=g)
+            x.grad = gr.clone()
+            y.grad.copy_(gr)
+        torch.nn.utils.clip_grad_norm_(list(pa.parameters()), 0.5)
+        oa.step()
+        adam()
+        torch.cuda.synchronize()
+        for x, y in zip(pa.parameters(), pb.parameters()):
+            sa, sb = oa.state[x], ob.state[y]
+            assert float(sa["step"]) == float(sb["step"]) == step + 1
+            assert (x - y).abs().max().item() <= 1e-6 * max(1.0, x.abs().max().item())
+            assert torch.allclose(x.grad, y.grad, rtol=1e-5, atol=1e-9)
+            assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=1e-5, atol=1e-9)
+            assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-12)
