@@ -526,6 +526,7 @@ def sb3_legs(dev, n, steps):
     from rl_rocket_amd.params import ENV_CONFIG_6DOF, MAX_EPISODE_STEPS
     from rl_rocket_amd.vec_env import RocketVecEnv
 
+    WARM_SB3 = 100
     out = {}
     rng = np.random.default_rng(0)
     host_pool = [rng.uniform(-1, 1, (n, 3)).astype(np.float32) for _ in range(POOL)]
@@ -543,9 +544,12 @@ def sb3_legs(dev, n, steps):
     venv = RocketVecEnv(n, model="6DOF", device=dev, max_episode_steps=MAX_EPISODE_STEPS, monitor=True,
                         **ENV_CONFIG_6DOF)
     venv.reset()
-    run(venv, host_pool, 0, 30)
+    # 100 warm-up steps: in the first ~100 steps after an env is created the host's synchronize
+    # sporadically waits several ms while the device time of the step stays ~50 us (HIP events,
+    # tools/probe_vecenv_host.py; profiles/r03/vh/): a region that starts earlier measures those
+    run(venv, host_pool, 0, WARM_SB3)
     t0 = time.perf_counter()
-    n_done = run(venv, host_pool, 30, steps)
+    n_done = run(venv, host_pool, WARM_SB3, steps)
     dt = time.perf_counter() - t0
     venv.timing = {}
     run(venv, host_pool, 0, steps)
@@ -561,16 +565,16 @@ def sb3_legs(dev, n, steps):
         "path": "RocketVecEnv(monitor=True).step(numpy actions) -> numpy obs/reward/done + lazy infos (SB3 VecEnv)"}
 
     # device outputs: device actions in, device tensors out (obs stay in HBM); with Monitor (every
-    # step's infos built two steps later) and without (nothing leaves HBM unless read). 60 warm-up
-    # steps: the first device-output steps pay one-time pinned-buffer / allocator costs
+    # step's infos built two steps later) and without (nothing leaves HBM unless read). The same
+    # warm-up (the first device-output steps also pay one-time pinned-buffer / allocator costs)
     pool = torch.rand((POOL, n, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(1)) * 2 - 1
     for mon in (True, False):
         venv = RocketVecEnv(n, model="6DOF", device=dev, max_episode_steps=MAX_EPISODE_STEPS, monitor=mon,
                             device_outputs=True, **ENV_CONFIG_6DOF)
         venv.reset()
-        run(venv, pool, 0, 60, host=False)
+        run(venv, pool, 0, WARM_SB3, host=False)
         t0 = time.perf_counter()
-        run(venv, pool, 60, steps, host=False)
+        run(venv, pool, WARM_SB3, steps, host=False)
         dt = time.perf_counter() - t0
         venv.timing = {}
         run(venv, pool, 0, steps, host=False)
