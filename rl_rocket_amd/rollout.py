@@ -661,7 +661,9 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
 class GraphedPPOUpdate:
     """``ppo_update``'s minibatch step — gather, forward, clipped-surrogate / value / entropy
     loss, backward, (multi-GPU gradient all_reduce), grad-norm clip, Adam step — captured ONCE
-    into a hipGraph and replayed per minibatch.
+    into a hipGraph — one graph per EPOCH: the minibatch steps of one pass over the rollout,
+    each reading its rows from a static permutation buffer that ``update`` refills with
+    ``torch.randperm`` before every replay (no per-minibatch index copy or graph launch).
 
     ``fused`` (default: wherever ``PPOGrad`` supports the policy) takes the loss + backward from
     ``PPOGrad`` (rr_ppo_grad: one fp32-MFMA HIP pipeline) instead of PyTorch autograd, whose
@@ -698,7 +700,8 @@ class GraphedPPOUpdate:
         self.adv_all = ro.advantages.reshape(n)
         self.ret = ro.returns.reshape(n)
         self.coef = (clip_range, ent_coef, vf_coef, max_grad_norm)
-        self.idx = torch.arange(batch_size, device=dev)
+        self.perm = torch.arange(n, device=dev)  # refilled per epoch; minibatch k = perm[k bs : (k + 1) bs]
+        self.n_mb = n // batch_size
         params = list(policy.parameters())
         # state to restore after the warm-up steps (in place: the graph keeps these tensors)
         saved_p = [p.detach().clone() for p in params]
@@ -707,8 +710,7 @@ class GraphedPPOUpdate:
         # static gradient buffers (allocated outside the graph): the captured step copies
         # torch.autograd.grad's results into them, so no accumulation into .grad is captured. The
         # policy's Linear layers must take their bias gradient as a GEMM (_LinearFn): a column sum
-        # after a GEMM in the same graph is wrong from the second replay on (tools/dbg_graphed_update.py,
-        # tools/probe_graph_reduce.py)
+        # after a GEMM in the same graph is wrong from the second replay on (tools/probe_graph_reduce.py)
         self.params = params
         for p in params:
             p.grad = torch.zeros_like(p)
@@ -721,12 +723,13 @@ class GraphedPPOUpdate:
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
-            for _ in range(3):
-                self._step()
+            for k in range(3):
+                self._step(self._mb(k % self.n_mb))
         torch.cuda.current_stream(dev).wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.stats = self._step()
+            for k in range(self.n_mb):
+                self.stats = self._step(self._mb(k))
         with torch.no_grad():
             for p, v in zip(params, saved_p):
                 p.copy_(v)
@@ -743,9 +746,12 @@ class GraphedPPOUpdate:
                             v.zero_()  # state the warm-up created: back to a fresh optimizer's
         torch.cuda.synchronize(dev)
 
-    def _step(self):
+    def _mb(self, k):
+        return self.perm[k * self.bs:(k + 1) * self.bs]
+
+    def _step(self, i):
         clip_range, ent_coef, vf_coef, max_grad_norm = self.coef
-        pol, i = self.policy, self.idx
+        pol = self.policy
         if self.fused:
             st = self._grad(i)
             if self.group is not None:
@@ -779,8 +785,6 @@ class GraphedPPOUpdate:
         if self._adam is not None:
             self._adam.sync_lr()  # the graph reads lr from the device: follow param_groups[0]["lr"]
         for _ in range(n_epochs):
-            perm = torch.randperm(self.n, device=self.obs.device, generator=generator)
-            for s in range(0, self.n, self.bs):
-                self.idx.copy_(perm[s:s + self.bs])
-                self.graph.replay()
+            self.perm.copy_(torch.randperm(self.n, device=self.obs.device, generator=generator))
+            self.graph.replay()
         return {k: float(v) for k, v in self.stats.items()}

@@ -1,6 +1,7 @@
 """Time the PPO learner pieces on synthetic data of the configs[4] shape (16 x 65 536 samples,
 minibatch 65 536, 6DOF MlpPolicy): rr_ppo_grad per call, rr_clip_adam per call, and the graphed
-fused minibatch step (GraphedPPOUpdate), by HIP events over back-to-back calls.
+fused update (GraphedPPOUpdate: one graph per epoch, reported per minibatch), by HIP events over
+back-to-back calls.
 
     python tools/probe_ppo_grad.py [--calls 50] [--only grad]   (--only grad: the rocprofv3 --pmc runs)
 """
@@ -54,9 +55,9 @@ def main():
         out["clip_adam_us"] = events(adam, a.calls)
         opt2 = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5, capturable=True)
         g = GraphedPPOUpdate(pol, opt2, ro, batch_size=n, fused=True)
-        out["graphed_minibatch_us"] = events(g.graph.replay, a.calls)
+        out["graphed_minibatch_us"] = events(g.graph.replay, max(3, a.calls // g.n_mb)) / g.n_mb
         gt = GraphedPPOUpdate(pol, opt2, ro, batch_size=n, fused=False)
-        out["graphed_autograd_minibatch_us"] = events(gt.graph.replay, max(5, a.calls // 10))
+        out["graphed_autograd_minibatch_us"] = events(gt.graph.replay, 3) / gt.n_mb
     print(json.dumps(out))
 
 
