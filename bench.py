@@ -512,6 +512,35 @@ def cpu_baselines(model, seconds, cores):
 # ---------------------------------------------------------------------------------------------
 # wall-clock legs through the Python boundary (what SB3 calls)
 # ---------------------------------------------------------------------------------------------
+def _host_cpu():
+    """(process CPU seconds, cgroup CPU-throttled microseconds or None, threads) — evidence for
+    host-side stalls in the SB3-facing legs (a throttled cgroup stalls the stepping thread)."""
+    t = os.times()
+    thr = None
+    for path in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat", "/sys/fs/cgroup/cpu,cpuacct/cpu.stat"):
+        try:
+            kv = dict(line.split() for line in open(path) if line.strip())
+        except OSError:
+            continue
+        if "throttled_usec" in kv:
+            thr = int(kv["throttled_usec"])
+        elif "throttled_time" in kv:
+            thr = int(kv["throttled_time"]) // 1000
+        break
+    threads = None
+    try:
+        threads = int([x for x in open("/proc/self/status") if x.startswith("Threads:")][0].split()[1])
+    except (OSError, IndexError, ValueError):
+        pass
+    return t.user + t.system, thr, threads
+
+
+def _host_delta(a, b, dt):
+    return {"process_cpu_per_wall": round((b[0] - a[0]) / dt, 3),
+            "cgroup_throttled_ms": None if a[1] is None or b[1] is None else round((b[1] - a[1]) / 1e3, 1),
+            "threads": b[2]}
+
+
 def sb3_legs(dev, n, steps):
     """env-steps/s through the drop-in surface, wall clock, Monitor on, random actions:
     RocketVecEnv.step with host (numpy) outputs — what SB3's DummyVecEnv.step_wait returns,
@@ -548,16 +577,18 @@ def sb3_legs(dev, n, steps):
     # sporadically waits several ms while the device time of the step stays ~50 us (HIP events,
     # tools/probe_vecenv_host.py; profiles/r03/vh/): a region that starts earlier measures those
     run(venv, host_pool, 0, WARM_SB3)
+    h0 = _host_cpu()
     t0 = time.perf_counter()
     n_done = run(venv, host_pool, WARM_SB3, steps)
     dt = time.perf_counter() - t0
+    host = _host_delta(h0, _host_cpu(), dt)
     venv.timing = {}
     run(venv, host_pool, 0, steps)
     split = {k: v / steps * 1e6 for k, v in venv.timing.items()}
     venv.close()
     out["vecenv_host"] = {
         "value": n * steps / dt, "unit": "env-steps/s", "us_per_step": dt / steps * 1e6, "n_envs": n, "steps": steps,
-        "done_per_step": n_done / steps,
+        "done_per_step": n_done / steps, "host": host,
         "split_us_per_step": split,
         "split_note": "second pass with a synchronize after the launch: launch = action H2D + rr_step call (host), "
                       "kernel = remaining device time, d2h = obs / reward / done copies to numpy, infos = done list "
