@@ -25,7 +25,8 @@
  *
  * Conventions
  *   - All data pointers are DEVICE pointers (e.g. torch.Tensor.data_ptr()) on the
- *     handle's device, owned by the caller unless stated otherwise.
+ *     handle's device, or pinned host memory from rr_host_alloc (zero-copy: the kernels read
+ *     and write it directly), owned by the caller unless stated otherwise.
  *   - Every call is asynchronous on the given hipStream_t (pass as void*; NULL = the
  *     default stream). Apart from rr_fetch_done (documented as synchronising), no call
  *     synchronises, allocates or frees after rr_create, so rr_step / rr_reset can be
@@ -42,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 8
+#define RR_ABI_VERSION 9
 
 /* error codes */
 #define RR_OK 0
@@ -72,6 +73,13 @@ extern "C" {
 #define RR_FLAG_ACTION_SOA 0x8        /* action laid out [n_act][N] instead of [N][n_act] */
 #define RR_FLAG_SCIPY_H0_CLAMP 0x10   /* DOPRI5: scipy >= 1.12 select_initial_step (clamp h0 to
                                          the interval); default = scipy 1.7 (requirements.txt:73) */
+#define RR_FLAG_HOST_STATE 0x20       /* the state planes (+ v0, counter words, episode returns) live in
+                                         pinned, GPU-coherent host memory instead of HBM: after the
+                                         stream is synchronised the host reads them through
+                                         rr_get_buffers with no copy. For small N — the single-env gym
+                                         shims (rocket_env.py:690-719 called once per env step), whose
+                                         step is then one launch + one synchronise with the action and
+                                         outputs in rr_host_alloc memory */
 
 #define RR_MAX_STATE 14
 
@@ -198,6 +206,13 @@ int rr_set_aux(rr_env* e, const uint32_t* counter, const float* ep_return, void*
 
 /* Pointers to the library-owned buffers (done list of the last step, etc.). */
 int rr_get_buffers(rr_env* e, rr_buffers* out);
+
+/* Pinned, GPU-coherent (fine-grained) host memory that the kernels read and write directly:
+ * zero-copy step inputs / outputs for small N (the single-env gym shims pass the action and
+ * every output of rr_step in it, so a step needs no copy command). Host-only, synchronous;
+ * free with rr_host_free. */
+int rr_host_alloc(void** out, int64_t bytes);
+int rr_host_free(void* p);
 
 /* Host-side retrieval of the last step's done list (SB3 infos: terminal_observation,
  * Monitor episode stats). SYNCHRONISES `stream`. Writes at most `capacity` rows into

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
@@ -24,6 +24,7 @@ RR_FLAG_EPISODE_STATS = 0x2
 RR_FLAG_REWARD_ANNEALING = 0x4
 RR_FLAG_ACTION_SOA = 0x8
 RR_FLAG_SCIPY_H0_CLAMP = 0x10
+RR_FLAG_HOST_STATE = 0x20
 RR_MAX_STATE = 14
 RR_POLICY_FP32, RR_POLICY_BF16, RR_POLICY_FP16X3 = 0, 1, 2
 
@@ -103,6 +104,8 @@ SIGNATURES = {
     "rr_get_aux": (ctypes.c_int, [_P, _P, _P, _P]),
     "rr_set_aux": (ctypes.c_int, [_P, _P, _P, _P]),
     "rr_get_buffers": (ctypes.c_int, [_P, ctypes.POINTER(RrBuffers)]),
+    "rr_host_alloc": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int64]),
+    "rr_host_free": (ctypes.c_int, [_P]),
     "rr_fetch_done": (ctypes.c_int64, [_P, ctypes.c_int64, _P, _P, _P, _P, _P]),
     "rr_copy_terminal": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "rr_policy_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),

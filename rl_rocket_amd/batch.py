@@ -17,10 +17,43 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def _host_view(addr, shape, dtype):
+    """numpy array over `addr` (memory the library owns; valid while it does)."""
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    return np.frombuffer((ctypes.c_char * nbytes).from_address(addr), dtype=dtype).reshape(shape)
+
+
+class HostArray:
+    """A numpy array in pinned, GPU-coherent host memory (``rr_host_alloc``) that the kernels
+    read and write directly: zero-copy step inputs / outputs for small N (``ptr`` is what the
+    C-ABI takes). Freed by ``free()`` (or when collected); views of ``array`` must not outlive it."""
+
+    def __init__(self, shape, dtype):
+        self._lib = _lib.load()
+        nbytes = max(1, int(np.prod(shape)) * np.dtype(dtype).itemsize)
+        p = ctypes.c_void_p()
+        _lib.check(self._lib.rr_host_alloc(ctypes.byref(p), nbytes), "rr_host_alloc")
+        self.ptr = p
+        self.array = _host_view(p.value, shape, dtype)
+
+    def free(self):
+        if getattr(self, "ptr", None) is not None and self.ptr.value:
+            self.array = None
+            self._lib.rr_host_free(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class RocketBatch:
     def __init__(self, num_envs, model="6DOF", device=None, max_episode_steps=0, auto_reset=True,
                  episode_stats=True, reward_annealing=False, integrator="rk4", env_id_offset=0,
-                 compute_terms=False, seed=None, scipy_h0_clamp=False, action_soa=False, **env_kwargs):
+                 compute_terms=False, seed=None, scipy_h0_clamp=False, action_soa=False, host_state=False,
+                 **env_kwargs):
         import torch
 
         self.torch = torch
@@ -40,7 +73,10 @@ class RocketBatch:
         self.n_terms = len(self.cfg.term_names)
         self.params = lower(self.cfg, max_episode_steps=max_episode_steps, auto_reset=auto_reset,
                             episode_stats=episode_stats, reward_annealing=reward_annealing, integrator=integrator,
-                            scipy_h0_clamp=scipy_h0_clamp, action_soa=action_soa)
+                            scipy_h0_clamp=scipy_h0_clamp, action_soa=action_soa, host_state=host_state)
+        # host_state: the state planes (+ v0, counter words, returns) in pinned host memory
+        # (RR_FLAG_HOST_STATE), readable through host_state_arrays() after a stream synchronise
+        self.host_state = bool(host_state)
         # action_soa: step() takes actions as [action_dim][N] planes (RR_FLAG_ACTION_SOA)
         self.action_soa = bool(action_soa)
         self.lib = _lib.load()
@@ -176,6 +212,18 @@ class RocketBatch:
         el = t.empty((self.num_envs,), dtype=t.int32, device=self.device)
         _lib.check(self.lib.rr_get_state(self._h, _ptr(st), _ptr(v), _ptr(el), self._stream()), "rr_get_state")
         return st, v, el
+
+    def host_state_arrays(self):
+        """(state [state_dim][N] f32, v0 [N] f32, counter words [N] u32) as numpy views of the
+        library's pinned host planes (host_state=True only). They reflect the last step once the
+        stream has been synchronised; valid until close()."""
+        if not self.host_state:
+            raise ValueError("host_state_arrays() needs RocketBatch(host_state=True)")
+        b = _lib.RrBuffers()
+        _lib.check(self.lib.rr_get_buffers(self._h, ctypes.byref(b)), "rr_get_buffers")
+        n, ns = self.num_envs, self.state_dim
+        return (_host_view(b.state, (ns, n), np.float32), _host_view(b.v0, (n,), np.float32),
+                _host_view(b.elapsed, (n,), np.uint32))
 
     # -- counter words and checkpoints ---------------------------------------------------------------------------
     @property

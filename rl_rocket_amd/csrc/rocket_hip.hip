@@ -1495,6 +1495,7 @@ struct rr_env {
     float* term_ret;
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
+    bool host_state;    // RR_FLAG_HOST_STATE: `state` (+ v0, counter, ep_ret planes) is pinned host memory
     KParams* d_kp;      // device copy of kp (Bufs.kp)
     XParams* d_xp;      // device copy of xp (RR_INT_DOPRI5: step_exact_kernel reads it where it uses it)
     int32_t* g_idx;     // rr_fetch_done scratch
@@ -1588,7 +1589,20 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
     };
     const bool exact = p->integrator == RR_INT_DOPRI5;
+    e->host_state = (p->flags & RR_FLAG_HOST_STATE) != 0;
     for (auto& a : allocs) {
+        if (e->host_state && a.ptr == (void**)&e->state) {
+            // fine-grained (coherent) pinned host memory: the kernels' loads and stores go straight
+            // to host memory, and the host reads the planes after a stream synchronise
+            hipError_t err = hipHostMalloc(a.ptr, a.bytes, hipHostMallocCoherent | hipHostMallocMapped);
+            if (err != hipSuccess) {
+                *a.ptr = nullptr;
+                rr_destroy(e);
+                return hip_fail(err, "rr_create: hipHostMalloc (host state)");
+            }
+            std::memset(*a.ptr, 0, a.bytes);
+            continue;
+        }
         hipError_t err = hipMalloc(a.ptr, a.bytes);
         if (err != hipSuccess) {
             rr_destroy(e);
@@ -1639,6 +1653,10 @@ int rr_destroy(rr_env* e)
 {
     if (!e) return RR_OK;
     DeviceGuard g(e->device);
+    if (e->host_state && e->state) {
+        (void)hipHostFree(e->state);
+        e->state = nullptr;
+    }
     void* ptrs[] = {e->state, e->state64, e->d_kp, e->d_xp, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
     for (void* q : ptrs)
@@ -1796,10 +1814,10 @@ namespace {
 hipError_t set_aux(rr_env* e, const float* v0, const int32_t* elapsed, hipStream_t s)
 {
     hipError_t err = hipSuccess;
-    if (v0) err = hipMemcpyAsync(e->v0, v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    if (v0) err = hipMemcpyAsync(e->v0, v0, sizeof(float) * e->n, hipMemcpyDefault, s);
     if (err == hipSuccess) {
         if (elapsed) {
-            err = hipMemcpyAsync(e->counter, elapsed, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+            err = hipMemcpyAsync(e->counter, elapsed, sizeof(int32_t) * e->n, hipMemcpyDefault, s);
         } else {  // elapsed steps -> 0, the episode field (reset-stream key) is kept
             hipLaunchKernelGGL(clear_elapsed_kernel, dim3(grid_of(e->n)), dim3(kBlock), 0, s, e->counter, e->n,
                                e->kp.el_mask);
@@ -1813,9 +1831,9 @@ hipError_t set_aux(rr_env* e, const float* v0, const int32_t* elapsed, hipStream
 hipError_t get_aux(rr_env* e, float* v0, int32_t* elapsed, hipStream_t s)
 {
     hipError_t err = hipSuccess;
-    if (v0) err = hipMemcpyAsync(v0, e->v0, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+    if (v0) err = hipMemcpyAsync(v0, e->v0, sizeof(float) * e->n, hipMemcpyDefault, s);
     if (err == hipSuccess && elapsed)
-        err = hipMemcpyAsync(elapsed, e->counter, sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, s);
+        err = hipMemcpyAsync(elapsed, e->counter, sizeof(int32_t) * e->n, hipMemcpyDefault, s);
     return err;
 }
 
@@ -1838,7 +1856,7 @@ int rr_set_state(rr_env* e, const float* state_soa, const float* v0, const int32
     if (!e || !state_soa) return fail(RR_EINVAL, "rr_set_state: null argument");
     hipStream_t s = (hipStream_t)stream;
     const int64_t cnt = (int64_t)e->ns * e->n;
-    hipError_t err = hipMemcpyAsync(e->state, state_soa, sizeof(float) * cnt, hipMemcpyDeviceToDevice, s);
+    hipError_t err = hipMemcpyAsync(e->state, state_soa, sizeof(float) * cnt, hipMemcpyDefault, s);
     if (err == hipSuccess && e->state64) err = widen_async(e->state, e->state64, cnt, s);
     if (err == hipSuccess) err = set_aux(e, v0, elapsed, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_set_state");
@@ -1850,7 +1868,7 @@ int rr_get_state(rr_env* e, float* state_soa, float* v0, int32_t* elapsed, void*
     hipStream_t s = (hipStream_t)stream;
     hipError_t err = hipSuccess;
     if (state_soa)
-        err = hipMemcpyAsync(state_soa, e->state, sizeof(float) * e->ns * e->n, hipMemcpyDeviceToDevice, s);
+        err = hipMemcpyAsync(state_soa, e->state, sizeof(float) * e->ns * e->n, hipMemcpyDefault, s);
     if (err == hipSuccess) err = get_aux(e, v0, elapsed, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_get_state");
 }
@@ -1862,7 +1880,7 @@ int rr_set_state64(rr_env* e, const double* state_soa, const float* v0, const in
     const int64_t cnt = (int64_t)e->ns * e->n;
     hipError_t err = hipSuccess;
     if (e->state64) {
-        err = hipMemcpyAsync(e->state64, state_soa, sizeof(double) * cnt, hipMemcpyDeviceToDevice, s);
+        err = hipMemcpyAsync(e->state64, state_soa, sizeof(double) * cnt, hipMemcpyDefault, s);
         if (err == hipSuccess) err = narrow_async(e->state64, e->state, cnt, s);
     } else {
         err = narrow_async(state_soa, e->state, cnt, s);
@@ -1879,7 +1897,7 @@ int rr_get_state64(rr_env* e, double* state_soa, float* v0, int32_t* elapsed, vo
     hipError_t err = hipSuccess;
     if (state_soa) {
         if (e->state64)
-            err = hipMemcpyAsync(state_soa, e->state64, sizeof(double) * cnt, hipMemcpyDeviceToDevice, s);
+            err = hipMemcpyAsync(state_soa, e->state64, sizeof(double) * cnt, hipMemcpyDefault, s);
         else
             err = widen_async(e->state, state_soa, cnt, s);
     }
@@ -1894,9 +1912,9 @@ int rr_get_aux(rr_env* e, uint32_t* counter, float* ep_return, void* stream)
     if (!e) return fail(RR_EINVAL, "rr_get_aux: null handle");
     hipStream_t s = (hipStream_t)stream;
     hipError_t err = hipSuccess;
-    if (counter) err = hipMemcpyAsync(counter, e->counter, sizeof(uint32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    if (counter) err = hipMemcpyAsync(counter, e->counter, sizeof(uint32_t) * e->n, hipMemcpyDefault, s);
     if (err == hipSuccess && ep_return)
-        err = hipMemcpyAsync(ep_return, e->ep_ret, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+        err = hipMemcpyAsync(ep_return, e->ep_ret, sizeof(float) * e->n, hipMemcpyDefault, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_get_aux");
 }
 
@@ -1905,9 +1923,9 @@ int rr_set_aux(rr_env* e, const uint32_t* counter, const float* ep_return, void*
     if (!e) return fail(RR_EINVAL, "rr_set_aux: null handle");
     hipStream_t s = (hipStream_t)stream;
     hipError_t err = hipSuccess;
-    if (counter) err = hipMemcpyAsync(e->counter, counter, sizeof(uint32_t) * e->n, hipMemcpyDeviceToDevice, s);
+    if (counter) err = hipMemcpyAsync(e->counter, counter, sizeof(uint32_t) * e->n, hipMemcpyDefault, s);
     if (err == hipSuccess && ep_return)
-        err = hipMemcpyAsync(e->ep_ret, ep_return, sizeof(float) * e->n, hipMemcpyDeviceToDevice, s);
+        err = hipMemcpyAsync(e->ep_ret, ep_return, sizeof(float) * e->n, hipMemcpyDefault, s);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_set_aux");
 }
 
@@ -1923,6 +1941,26 @@ int rr_get_buffers(rr_env* e, rr_buffers* out)
     out->terminal_return = e->term_ret;
     out->terminal_len = e->term_len;
     return RR_OK;
+}
+
+int rr_host_alloc(void** out, int64_t bytes)
+{
+    if (!out || bytes <= 0) return fail(RR_EINVAL, "rr_host_alloc: null pointer or bytes <= 0");
+    *out = nullptr;
+    const hipError_t err = hipHostMalloc(out, (size_t)bytes, hipHostMallocCoherent | hipHostMallocMapped);
+    if (err != hipSuccess) {
+        *out = nullptr;
+        return hip_fail(err, "rr_host_alloc");
+    }
+    std::memset(*out, 0, (size_t)bytes);
+    return RR_OK;
+}
+
+int rr_host_free(void* p)
+{
+    if (!p) return RR_OK;
+    const hipError_t err = hipHostFree(p);
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_host_free");
 }
 
 int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs, float* term_return,

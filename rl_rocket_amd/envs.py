@@ -8,12 +8,17 @@ reference (SB3 ``check_env``, ``RewardAnnealing``, ``EpisodeAnalyzer``-style rea
 
 Reset draws the initial condition on the host with gym 0.21's ``Box.sample`` and seeding
 (``gym_compat``), i.e. the reference's own reset stream, and uploads it with
-``rr_set_state``; every ``step`` is one launch of the fused kernel.  Rendering (pygame /
+``rr_set_state``; every ``step`` is one launch of the fused kernel and one stream synchronise:
+the env's state lives in pinned host memory (``RR_FLAG_HOST_STATE``) and the action and outputs
+in ``rr_host_alloc`` memory, so the kernel reads and writes them in place (no copy commands).  Rendering (pygame /
 pyvista, rocket_env.py:249-383, 721-823) is out of scope and raises.
 """
+import ctypes
+
 import numpy as np
 
-from .batch import RocketBatch
+from . import _lib
+from .batch import HostArray, RocketBatch
 from .gym_compat import Box, EnvBase
 from .params import (ACTION_NAMES_3DOF, ACTION_NAMES_6DOF, MAX_GIMBAL, MAX_THRUST, STATE_NAMES_3DOF,
                      STATE_NAMES_6DOF, config_3dof, config_6dof)
@@ -55,8 +60,17 @@ class _RocketBase(EnvBase):
         self.infos = []
         self.SIM = None
         self.vtarg_history = []
+        # one step = one launch + one stream synchronise: the env's state planes live in pinned
+        # host memory (RR_FLAG_HOST_STATE) and the action and every output in rr_host_alloc
+        # memory, so the kernel reads and writes them directly and no copy command is queued
         self._batch = RocketBatch(1, model=cfg.model, device=device, max_episode_steps=0, auto_reset=False,
-                                  episode_stats=False, compute_terms=True, **kw)
+                                  episode_stats=False, compute_terms=True, host_state=True, **kw)
+        nt = len(cfg.term_names)
+        self._io = {k: HostArray(shape, dt) for k, shape, dt in (
+            ("action", (1, na), np.float32), ("obs", (1, ns), np.float32), ("reward", (1,), np.float32),
+            ("done", (1,), np.uint8), ("terms", (nt + 2, 1), np.float32))}
+        self._state_h = self._batch.host_state_arrays()[0]
+        self._torch = self._batch.torch
 
     # -- gym API ----------------------------------------------------------------------------------------------
     def seed(self, seed: int = 42):
@@ -73,27 +87,25 @@ class _RocketBase(EnvBase):
                               v0=torch.tensor([v0], dtype=torch.float32))
 
     def _step_device(self, a):
-        import torch
-
-        obs, rew, done, _ = self._batch.step(torch.from_numpy(a.reshape(1, -1)))
-        st = self._batch.get_state()[0]
-        packed = torch.cat([obs.reshape(-1), rew.reshape(-1), done.float().reshape(-1),
-                            self._batch.terms.reshape(-1), st.reshape(-1)]).cpu().numpy()
-        ns, nt = self.cfg.state_dim, len(self.cfg.term_names)
-        o = 0
-        obs_h = packed[o:o + ns].astype(np.float32); o += ns
-        rew_h = float(packed[o]); o += 1
-        done_h = bool(packed[o] > 0.5); o += 1
-        terms = packed[o:o + nt + 2]; o += nt + 2
-        state = packed[o:o + ns].astype(np.float64)
-        return obs_h, rew_h, done_h, terms, state
+        io, b = self._io, self._batch
+        io["action"].array[0] = a
+        stream = self._torch.cuda.current_stream(b.device)
+        _lib.check(b.lib.rr_step(b._h, io["action"].ptr, io["obs"].ptr, io["reward"].ptr, io["done"].ptr, None,
+                                 io["terms"].ptr, ctypes.c_void_p(stream.cuda_stream)), "rr_step")
+        stream.synchronize()
+        return (io["obs"].array[0].copy(), float(io["reward"].array[0]), bool(io["done"].array[0]),
+                io["terms"].array[:, 0].copy(), self._state_h[:, 0].astype(np.float64))
 
     def render(self, mode="human"):
         raise NotImplementedError("rendering (pygame / pyvista) is out of scope of rl_rocket_amd")
 
     def close(self):
         if getattr(self, "_batch", None) is not None:
-            self._batch.close()
+            self._batch.close()  # synchronises the device: no kernel still uses the host buffers
+            self._batch = None
+            self._state_h = None
+            for h in self._io.values():
+                h.free()
 
     def used_mass(self):
         return self.SIM.states[0][-1] - self.SIM.states[-1][-1]

@@ -185,7 +185,7 @@ INTEGRATORS = {"rk4": _lib.RR_INT_RK4, "euler": _lib.RR_INT_EULER, "dopri5": _li
 
 
 def lower(cfg, max_episode_steps=0, auto_reset=True, episode_stats=True, reward_annealing=False,
-          integrator="rk4", action_soa=False, xi_default=0.01, scipy_h0_clamp=False):
+          integrator="rk4", action_soa=False, xi_default=0.01, scipy_h0_clamp=False, host_state=False):
     """EnvConfig -> ctypes rr_params. ``integrator``: "rk4" (fast parity mode), "euler"
     (non-parity speed mode) or "dopri5" (exact mode: fp64 scipy RK45 restatement);
     ``scipy_h0_clamp`` selects scipy >= 1.12's select_initial_step in dopri5 mode."""
@@ -204,6 +204,8 @@ def lower(cfg, max_episode_steps=0, auto_reset=True, episode_stats=True, reward_
         flags |= _lib.RR_FLAG_ACTION_SOA
     if scipy_h0_clamp:
         flags |= _lib.RR_FLAG_SCIPY_H0_CLAMP
+    if host_state:
+        flags |= _lib.RR_FLAG_HOST_STATE
     p.flags = flags
     p.dt = float(cfg.kwargs["timestep"])
     ns = cfg.state_dim

@@ -434,3 +434,81 @@ def test_episode_analyzer_drop_in():
     assert isinstance(u.get_vtarg_trajectory(), go.Figure)
     assert isinstance(u.get_attitude_trajectory(), go.Figure)
     u.close()
+
+
+@pytest.mark.parametrize("model", [6, 3])
+def test_shim_zero_copy_step_is_bitwise_the_device_batch(model):
+    """The single-env shims step with their state in pinned host memory (RR_FLAG_HOST_STATE) and
+    the action / outputs in rr_host_alloc memory (one launch + one synchronise per step); the
+    same steps on a device-resident N = 1 batch give bitwise the same obs, reward, done, reward
+    terms and state, across episodes (resets re-inject the shim's own IC into the twin)."""
+    import torch
+
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.envs import Rocket, Rocket6DOF
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+
+    env = Rocket6DOF(**ENV_CONFIG_6DOF) if model == 6 else Rocket()
+    twin = RocketBatch(1, model=model, max_episode_steps=0, auto_reset=False, episode_stats=False,
+                       compute_terms=True, **env.cfg.kwargs)
+    ns, na = env.cfg.state_dim, env.cfg.action_dim
+    rng = np.random.default_rng(7)
+
+    def sync_twin():
+        torch.cuda.synchronize()
+        st, v0, _ = env._batch.host_state_arrays()
+        twin.set_state(torch.from_numpy(st.copy()), v0=torch.from_numpy(v0.copy()))
+
+    env.reset()
+    sync_twin()
+    episodes = 0
+    for k in range(300):
+        a = rng.uniform(-1, 1, na).astype(np.float32)
+        obs, reward, done, info = env.step(a)
+        o, r, d, _ = twin.step(torch.from_numpy(a.reshape(1, na)))
+        st = twin.get_state()[0]
+        torch.cuda.synchronize()
+        if model == 6:  # the 3DOF shim's obs is the reference's float64 obs, made on the host from the state
+            np.testing.assert_array_equal(obs, o.cpu().numpy()[0])
+        assert np.float32(reward) == r.cpu().numpy()[0]
+        assert done == bool(d.cpu().numpy()[0])
+        terms = twin.terms.cpu().numpy()[:, 0]
+        names = env.cfg.term_names
+        np.testing.assert_array_equal(np.float32([info["rewards_dict"][n] for n in names]), terms[:len(names)])
+        assert info["bounds_violation"] == bool(terms[len(names)] > 0.5)
+        np.testing.assert_array_equal(env.SIM.states[-1].astype(np.float32), st.cpu().numpy()[:, 0])
+        if done:
+            episodes += 1
+            env.reset()
+            sync_twin()
+    assert episodes >= 2
+    env.close()
+    twin.close()
+
+
+@pytest.mark.parametrize("n", [1000, 70000])
+def test_host_state_batch_is_bitwise_device_state(n):
+    """RR_FLAG_HOST_STATE at N > 1 (helper-wave and plain kernels, auto-reset, TimeLimit): the
+    same stepping as a device-state batch, bitwise, and the host views equal rr_get_state."""
+    import torch
+
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+
+    kw = dict(model="6DOF", max_episode_steps=15, auto_reset=True, episode_stats=True, **ENV_CONFIG_6DOF)
+    a, b = RocketBatch(n, host_state=True, **kw), RocketBatch(n, **kw)
+    a.reset(), b.reset()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for k in range(40):
+        act = torch.rand((n, 3), device="cuda", generator=g) * 2 - 1
+        oa, ra, da, ta = (x.clone() for x in a.step(act))
+        ob, rb, db, tb = b.step(act)
+        for x, y in ((oa, ob), (ra, rb), (da, db), (ta, tb)):
+            assert torch.equal(x, y)
+    torch.cuda.synchronize()
+    st, v0, cw = a.host_state_arrays()
+    sb, vb, eb = b.get_state()
+    np.testing.assert_array_equal(st, sb.cpu().numpy())
+    np.testing.assert_array_equal(v0, vb.cpu().numpy())
+    np.testing.assert_array_equal(cw.view(np.int32), eb.cpu().numpy())
+    a.close(), b.close()
