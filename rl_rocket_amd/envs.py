@@ -59,7 +59,6 @@ class _RocketBase(EnvBase):
         self.action_space = Box(low=-1, high=1, shape=(na,)).to_gym()
         self.infos = []
         self.SIM = None
-        self.vtarg_history = []
         # one step = one launch + one stream synchronise: the env's state planes live in pinned
         # host memory (RR_FLAG_HOST_STATE) and the action and every output in rr_host_alloc
         # memory, so the kernel reads and writes them directly and no copy command is queued
@@ -123,6 +122,15 @@ class _RocketBase(EnvBase):
     def _get_normalizer(self):
         return self.state_normalizer
 
+    @property
+    def vtarg_history(self):
+        """v_targ of every step since the last reset. The reference appends it inside its reward
+        (rocket_env.py:1012 / :245); the kernel computes it there too but does not return it, so
+        here it is derived on access from the stored float32-cast states (``SIM.states``), the
+        same values, and a step pays nothing for it."""
+        sim = self.SIM
+        return [] if sim is None else [self._compute_vtarg(np.asarray(s, np.float32)) for s in sim.states[1:]]
+
 
 class Rocket6DOF(_RocketBase):
     """rocket_env.py:505 ``Rocket6DOF`` over the HIP step kernel."""
@@ -154,7 +162,6 @@ class Rocket6DOF(_RocketBase):
 
     def reset(self):
         """rocket_env.py:665-688"""
-        self.vtarg_history = []
         ic = self.init_space.sample()
         ic[6:10] = ic[6:10] / np.linalg.norm(ic[6:10])
         self.initial_condition = ic
@@ -174,7 +181,6 @@ class Rocket6DOF(_RocketBase):
         self.SIM.times.append(self.SIM.t)
         self.SIM.states.append(state)
         self.SIM.actions.append(self.action)
-        self.vtarg_history.append(self._compute_vtarg(state.astype(np.float32)))
         rewards_dict = {k: float(terms[j]) for j, k in enumerate(self.cfg.term_names)}
         info = {
             "rewards_dict": rewards_dict,
@@ -296,7 +302,6 @@ class Rocket(_RocketBase):
 
     def reset(self):
         """rocket_env.py:137-148 (returns a float64 observation, like the reference)"""
-        self.vtarg_history = []
         ic = self.init_space.sample()
         self.y = ic
         self.SIM = _SimView(ic, self.timestep, 2)
@@ -324,6 +329,26 @@ class Rocket(_RocketBase):
             "bounds_violation": bool(terms[len(self.cfg.term_names)] > 0.5),
         }
         return self._normalize_obs(state.astype(np.float32)), reward, done, info
+
+    def _compute_vtarg(self, state32):
+        """rocket_env.py:219-247 (host side, for vtarg_history only; z is the altitude, no +1)."""
+        r, v = state32[0:2], state32[3:5]
+        v_0 = np.linalg.norm(self.SIM.states[0][3:5])
+        if r[1] > self.waypoint:
+            r_hat = r - [0, self.waypoint]
+            v_hat = v - [0, -2]
+            tau = 20
+        else:
+            r_hat = [0, r[1]]
+            v_hat = v - [0, -1]
+            tau = 100
+        t_go = np.linalg.norm(r_hat) / np.linalg.norm(v_hat)
+        return -v_0 * (np.array(r_hat) / max(1e-3, np.linalg.norm(r_hat))) * (1 - np.exp(-t_go / tau))
+
+    def vtarg_to_dataframe(self):
+        import pandas as pd
+
+        return pd.DataFrame(self.vtarg_history, columns=["v_x", "v_y"])
 
     def _denormalize_action(self, action):
         """rocket_env.py:395-406 (no clipping)"""

@@ -65,7 +65,7 @@ def _stub_env(T=6):
 
     u.SIM = SIM()
     u.SIM.states, u.SIM.actions = states, [[0, 0, 0]] + [list(rng.normal(size=3)) for _ in range(T)]
-    u.vtarg_history = [rng.normal(size=3) for _ in range(T)]
+    u.waypoint = 50.0  # vtarg_history is derived from SIM.states (envs._RocketBase.vtarg_history)
     u.observation_space = u.action_space = None
     return u
 

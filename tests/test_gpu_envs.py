@@ -477,6 +477,12 @@ def test_shim_zero_copy_step_is_bitwise_the_device_batch(model):
         np.testing.assert_array_equal(np.float32([info["rewards_dict"][n] for n in names]), terms[:len(names)])
         assert info["bounds_violation"] == bool(terms[len(names)] > 0.5)
         np.testing.assert_array_equal(env.SIM.states[-1].astype(np.float32), st.cpu().numpy()[:, 0])
+        if k % 10 == 0:  # the host-derived v_targ history reproduces the kernel's velocity-tracking term
+            vt = env.vtarg_history
+            assert len(vt) == len(env.SIM.states) - 1
+            v = env.SIM.states[-1].astype(np.float32)[3:3 + (3 if model == 6 else 2)]
+            np.testing.assert_allclose(env.reward_coefficients["alfa"] * np.linalg.norm(v - vt[-1]),
+                                       info["rewards_dict"]["velocity_tracking"], rtol=1e-5, atol=1e-6)
         if done:
             episodes += 1
             env.reset()

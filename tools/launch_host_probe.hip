@@ -27,6 +27,15 @@ __global__ void empty_kernel(float* state, const float* action, uint32_t n, uint
     if (n == 0xFFFFFFFFu && threadIdx.x == 0) state[0] = b.f[mode & 63] + action[0];
 }
 
+// ~`mode` x 10 ns of wall time per wave (100 MHz realtime clock): keeps the GPU behind the host
+// so that launches queue up, as the step kernel's ~4.2 us do against ~2-5 us of host per launch
+__global__ void busy_kernel(float* state, const float* action, uint32_t n, uint32_t mode, Blob b)
+{
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < mode) __builtin_amdgcn_s_sleep(1);
+    if (n == 0xFFFFFFFFu && threadIdx.x == 0) state[0] = b.f[mode & 63] + action[0];
+}
+
 #define CK(x)                                                                     \
     do {                                                                          \
         hipError_t e_ = (x);                                                      \
@@ -85,6 +94,23 @@ int main()
         CK(hipStreamSynchronize(s));
         std::sort(us.begin(), us.end());
         std::printf(", \"%s_us\": %.3f", names[v], us[us.size() / 2]);
+    }
+    // busy kernels (~4 us each): does the host cost per launch grow when the queue backs up?
+    for (int kk : {20, 200}) {
+        for (uint32_t busy : {0u, 400u}) {
+            std::vector<double> us;
+            for (int r = 0; r < R + 2; ++r) {
+                CK(hipStreamSynchronize(s));
+                auto t0 = std::chrono::steady_clock::now();
+                for (int k = 0; k < kk; ++k)
+                    hipLaunchKernelGGL(busy_kernel, dim3(1024), dim3(256), 0, s, st, ac, n, busy, b);
+                auto t1 = std::chrono::steady_clock::now();
+                if (r >= 2) us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count() / kk);
+            }
+            CK(hipStreamSynchronize(s));
+            std::sort(us.begin(), us.end());
+            std::printf(", \"busy%u_K%d_us\": %.3f", busy, kk, us[us.size() / 2]);
+        }
     }
     std::printf("}\n");
     CK(hipGetLastError());

@@ -74,6 +74,19 @@ def part_a(dev, reps=30, K=20):
                      "wall_minus_events_us": med([r[0] - r[2] for r in rows]),
                      "per_step_wall_us": round(med([r[0] for r in rows]) / K, 3),
                      "per_step_events_us": round(med([r[2] for r in rows]) / K, 3)}
+    # host time of ONE rr_step call on an idle queue (ctypes call + launch), and of 20 back to back
+    P = __import__("ctypes").c_void_p
+    lib, h, sp = env.lib, env._h, P(torch.cuda.current_stream(dev).cuda_stream)
+    args = [P(pool[0].data_ptr()), P(env.obs.data_ptr()), P(env.reward.data_ptr()), P(env.done.data_ptr()),
+            P(env.truncated.data_ptr()), None, sp]
+    one = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lib.rr_step(h, *args)
+        one.append((time.perf_counter() - t0) * 1e6)
+    torch.cuda.synchronize()
+    out["rr_step_call_idle_queue_us"] = med(one)
     env.close()
     return out
 
