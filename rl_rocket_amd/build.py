@@ -32,7 +32,7 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def command(resource_usage=False, out=OUT, defines=(), extra=(), src=SRC, compile_only=False):
+def command(resource_usage=False, out=OUT, defines=(), extra=(), src=SRC, compile_only=False, preload=4):
     # -fno-slp-vectorize: the SLP pass packs scalar f32 math into v_pk_* pairs and adds ~180
     # register moves to the step kernel (measured on the .s); the scalar stream is shorter.
     # -ffp-contract=on: a*b+c becomes an fma only inside one source expression. HIP's default
@@ -42,8 +42,9 @@ def command(resource_usage=False, out=OUT, defines=(), extra=(), src=SRC, compil
     # contraction makes every kernel that inlines the physics compute the same bits.
     # kernarg preload: the step kernel's leading pointer / word arguments arrive in user SGPRs
     cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-fno-slp-vectorize", "-ffp-contract=on", "-std=c++17",
-           "-fPIC", "-c" if compile_only else "-shared", "-mllvm", "-amdgpu-kernarg-preload-count=4",
-           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")] + list(extra) + \
+           "-fPIC", "-c" if compile_only else "-shared"] + \
+        (["-mllvm", "-amdgpu-kernarg-preload-count=%d" % preload] if preload else []) + \
+        ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")] + list(extra) + \
         ["-D%s" % d for d in defines] + ["-o", out, src]
     if resource_usage:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
@@ -65,19 +66,20 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
-def commands(resource_usage=False, out=OUT, defines=(), extra=()):
+def commands(resource_usage=False, out=OUT, defines=(), extra=(), preload=4):
     """The three steps of the library build: the main translation unit and the exact-mode one
     compiled to objects (the latter with EXACT_FLAGS), then linked into `out`."""
     o_main, o_exact = out + ".main.o", out + ".exact.o"
-    c1 = command(resource_usage, o_main, defines, extra, SRC, compile_only=True)
-    c2 = command(resource_usage, o_exact, defines, list(extra) + EXACT_FLAGS, SRC_EXACT, compile_only=True)
+    c1 = command(resource_usage, o_main, defines, extra, SRC, compile_only=True, preload=preload)
+    c2 = command(resource_usage, o_exact, defines, list(extra) + EXACT_FLAGS, SRC_EXACT, compile_only=True,
+                 preload=preload)
     c3 = [hipcc(), "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-o", out, o_main, o_exact]
     return [c1, c2, c3]
 
 
-def build_lib(out=OUT, defines=(), extra=(), resource_usage=False, verbose=True):
+def build_lib(out=OUT, defines=(), extra=(), resource_usage=False, verbose=True, preload=4):
     """Compile both translation units (in parallel) and link `out`."""
-    c1, c2, c3 = commands(resource_usage, out, defines, extra)
+    c1, c2, c3 = commands(resource_usage, out, defines, extra, preload=preload)
     if verbose:
         for c in (c1, c2, c3):
             print("[rl_rocket_amd.build]", " ".join(c), flush=True)
