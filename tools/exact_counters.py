@@ -14,11 +14,13 @@ import os
 import statistics
 
 
-def counters(d):
+def counters(d, grid=None):
+    """Per-dispatch medians of the exact kernel's counters (only dispatches of `grid` threads when
+    given: bench.py's N sweep runs the same kernel at other N in the same process)."""
     out = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "step_exact" not in r["Kernel_Name"]:
+            if "step_exact" not in r["Kernel_Name"] or (grid and int(r["Grid_Size"]) != grid):
                 continue
             out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return {k: statistics.median(v) for k, v in out.items()}
@@ -29,21 +31,27 @@ def main():
     ap.add_argument("run_dir")
     ap.add_argument("--out")
     a = ap.parse_args()
-    c = {}
-    for sub in ("exact_SQ", "exact_SQ2"):
-        c.update(counters(os.path.join(a.run_dir, sub)))
-    res = {"median_per_dispatch": c}
-    stats = glob.glob(os.path.join(a.run_dir, "exact_kt", "**", "*kernel_stats.csv"), recursive=True)
-    for f in stats:
-        for r in csv.DictReader(open(f)):
-            if "step_exact" in r["Name"]:
-                res["kernel_trace"] = {"name": r["Name"], "calls": int(r["Calls"]), "mean_us": float(r["AverageNs"]) / 1e3,
-                                       "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3}
+    res = {}
+    n = None
     bench = os.path.join(a.run_dir, "bench_exact.json")
     if os.path.exists(bench):
         line = [json.loads(x) for x in open(bench) if x.startswith("{")][-1]
+        n = line["config"]["envs_per_gpu"]
         res["bench"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
-                        "kernel_us_events": line["roofline"]["kernel_us"], "n": line["config"]["envs_per_gpu"]}
+                        "kernel_us_events": line["roofline"]["kernel_us"], "n": n}
+    # dispatches at the bench's N only (one thread per env)
+    c = {}
+    for sub in ("exact_SQ", "exact_SQ2"):
+        c.update(counters(os.path.join(a.run_dir, sub), n))
+    res["median_per_dispatch"] = c
+    for f in glob.glob(os.path.join(a.run_dir, "exact_kt", "**", "*kernel_trace.csv"), recursive=True):
+        rows = [r for r in csv.DictReader(open(f)) if "step_exact" in r["Kernel_Name"] and
+                (n is None or int(r["Grid_Size_X"]) == n)]
+        if rows:
+            us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+            res["kernel_trace"] = {"name": rows[0]["Kernel_Name"], "calls": len(us), "grid": n,
+                                   "mean_us": statistics.mean(us), "median_us": statistics.median(us),
+                                   "min_us": min(us), "max_us": max(us)}
     w = c.get("SQ_WAVES")
     if w:
         d = {}

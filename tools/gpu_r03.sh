@@ -70,13 +70,13 @@ if has pmc; then
 fi
 if has exact; then
   # exact mode (fp64 DOPRI5 + brentq): wall clock, kernel trace and SQ counters of step_exact_kernel
-  step bench_exact 300 python "$R/bench.py" --integrator dopri5 --steps 200 --warmup 10 --no-cpu-baseline > "$OUT/bench_exact.json" 2> "$OUT/bench_exact.err"
+  step bench_exact 300 python "$R/bench.py" --integrator dopri5 --steps 200 --warmup 10 --no-cpu-baseline --n-sweep "" > "$OUT/bench_exact.json" 2> "$OUT/bench_exact.err"
   cat "$OUT/bench_exact.json"
   cd /tmp || exit 2
   mkdir -p "$OUT/exact_kt"
-  step exact_kt 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/exact_kt" -o bench -- python "$R/bench.py" --integrator dopri5 --steps 200 --warmup 10 --no-cpu-baseline > "$OUT/exact_kt/bench.json" 2>&1
-  step exact_SQ 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/exact_SQ" -o pmc -- python "$R/bench.py" --integrator dopri5 --steps 50 --warmup 5 --no-cpu-baseline > "$OUT/exact_SQ.log" 2>&1
-  step exact_SQ2 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_SMEM --output-format csv -d "$OUT/exact_SQ2" -o pmc -- python "$R/bench.py" --integrator dopri5 --steps 50 --warmup 5 --no-cpu-baseline > "$OUT/exact_SQ2.log" 2>&1
+  step exact_kt 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/exact_kt" -o bench -- python "$R/bench.py" --integrator dopri5 --steps 200 --warmup 10 --no-cpu-baseline --n-sweep "" > "$OUT/exact_kt/bench.json" 2>&1
+  step exact_SQ 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/exact_SQ" -o pmc -- python "$R/bench.py" --integrator dopri5 --steps 50 --warmup 5 --no-cpu-baseline --n-sweep "" > "$OUT/exact_SQ.log" 2>&1
+  step exact_SQ2 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_SMEM --output-format csv -d "$OUT/exact_SQ2" -o pmc -- python "$R/bench.py" --integrator dopri5 --steps 50 --warmup 5 --no-cpu-baseline --n-sweep "" > "$OUT/exact_SQ2.log" 2>&1
   cd "$R" || exit 2
 fi
 echo done
