@@ -289,19 +289,20 @@ class RocketBatch:
         return st, v, el
 
     def fetch_done(self, capacity=None):
-        """Done list of the last step on the host: (idx, terminal_obs, episode_return, episode_len).
-        Synchronises the stream."""
-        cap = self.num_envs if capacity is None else int(capacity)
-        idx = np.empty(cap, np.int32)
-        tobs = np.empty((cap, self.state_dim), np.float32)
-        ret = np.empty(cap, np.float32)
-        ln = np.empty(cap, np.int32)
-        c = self.lib.rr_fetch_done(self._h, cap, idx.ctypes.data_as(ctypes.c_void_p),
-                                   tobs.ctypes.data_as(ctypes.c_void_p), ret.ctypes.data_as(ctypes.c_void_p),
-                                   ln.ctypes.data_as(ctypes.c_void_p), self._stream())
+        """Done list of the last step on the host: (idx, terminal_obs, episode_return, episode_len),
+        fresh arrays of the done rows. Synchronises the stream. The rows land in persistent pinned
+        buffers (rr_host_alloc, allocated on the first call: the copies go straight to them instead
+        of through the runtime's staging of pageable memory) and are copied out."""
+        cap = self.num_envs if capacity is None else min(int(capacity), self.num_envs)
+        if getattr(self, "_fetch", None) is None:
+            n, ns = self.num_envs, self.state_dim
+            self._fetch = (HostArray((n,), np.int32), HostArray((n, ns), np.float32), HostArray((n,), np.float32),
+                           HostArray((n,), np.int32))
+        bufs = self._fetch
+        c = self.lib.rr_fetch_done(self._h, cap, *(b.ptr for b in bufs), self._stream())
         _lib.check(c, "rr_fetch_done")
         m = min(int(c), cap)
-        return idx[:m], tobs[:m], ret[:m], ln[:m]
+        return tuple(b.array[:m].copy() for b in bufs)
 
     def copy_terminal(self, out=None):
         """Device copies of the terminal rows of the envs done at the last step (rr_copy_terminal:
@@ -322,6 +323,9 @@ class RocketBatch:
             self.torch.cuda.synchronize(self.device)
             self.lib.rr_destroy(self._h)
             self._h = ctypes.c_void_p()
+        for b in getattr(self, "_fetch", None) or ():
+            b.free()
+        self._fetch = None
 
     def __del__(self):
         try:

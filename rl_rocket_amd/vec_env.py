@@ -44,11 +44,17 @@ class _DoneRows:
 
     def __init__(self, idx, tobs, ret, ln, trunc, max_episode_steps, monitor, stamp):
         self.idx = np.asarray(idx)
-        self.pos = dict(zip(self.idx.tolist(), range(len(self.idx))))
+        self._pos = None  # env index -> row, built on the first info() (most steps' infos are never read)
         self.tobs, self.ret, self.ln, self.trunc = tobs, ret, ln, trunc
         self.max_steps = max_episode_steps
         self.monitor = monitor
         self.stamp = stamp
+
+    @property
+    def pos(self):
+        if self._pos is None:
+            self._pos = dict(zip(self.idx.tolist(), range(len(self.idx))))
+        return self._pos
 
     def info(self, i):
         """SB3 DummyVecEnv + gym TimeLimit + Monitor info of done env i (None if not done)."""
@@ -208,10 +214,16 @@ class RocketVecEnv(_VecEnvBase):
             t1 = time.perf_counter()
             self.batch.torch.cuda.synchronize(self.batch.device)
             t2 = time.perf_counter()
+        # the three small outputs as asynchronous copies into persistent pinned buffers, then the
+        # observation's blocking copy (which synchronises the stream behind them): one host round
+        # trip instead of four
+        pin = self._pinned()
+        for dst, src in zip(pin, (rew, done, trunc)):
+            dst.copy_(src, non_blocking=True)
         obs_h = obs.cpu().numpy()
-        rew_h = rew.cpu().numpy()
-        done_h = done.cpu().numpy().astype(bool)
-        trunc_h = trunc.cpu().numpy()
+        rew_h = pin[0].numpy().copy()
+        done_h = pin[1].numpy().astype(bool)
+        trunc_h = pin[2].numpy().copy()
         if tm is not None:
             t3 = time.perf_counter()
         rows = None
@@ -229,6 +241,14 @@ class RocketVecEnv(_VecEnvBase):
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
+
+    def _pinned(self):
+        """Persistent pinned host buffers for reward, done and truncated (host outputs)."""
+        if getattr(self, "_pin", None) is None:
+            t, n = self.batch.torch, self.num_envs
+            self._pin = (t.empty((n,), dtype=t.float32, pin_memory=True), t.empty((n,), dtype=t.uint8, pin_memory=True),
+                         t.empty((n,), dtype=t.uint8, pin_memory=True))
+        return self._pin
 
     def _now(self):
         return round(time.time() - self._t_start, 6)
