@@ -37,7 +37,9 @@ def test_done_infos_match_sb3_semantics():
     env = _env()
     trunc = np.array([0, 1, 0, 0, 0], np.uint8)
     idx, tobs, ret, ln = env.batch.fetch_done()
-    infos = LazyInfos(5, env._done_rows(idx, tobs, ret, ln, trunc[idx], 1.5), None, ["a"])
+    rows = env._done_rows(idx, tobs, ret, ln, trunc[idx], 1.5)
+    assert rows._pos is None  # the env -> row map is built on the first infos access, not per step
+    infos = LazyInfos(5, rows, None, ["a"])
     assert len(infos) == 5
     assert infos[0] == {} and infos[2] == {} and infos[4] == {}
     assert infos[1]["TimeLimit.truncated"] is True
