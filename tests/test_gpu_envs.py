@@ -492,10 +492,11 @@ def test_shim_zero_copy_step_is_bitwise_the_device_batch(model):
     twin.close()
 
 
-@pytest.mark.parametrize("n", [1000, 70000])
+@pytest.mark.parametrize("n", [1000, 70000, 140000])
 def test_host_state_batch_is_bitwise_device_state(n):
-    """RR_FLAG_HOST_STATE at N > 1 (helper-wave and plain kernels, auto-reset, TimeLimit): the
-    same stepping as a device-state batch, bitwise, and the host views equal rr_get_state."""
+    """RR_FLAG_HOST_STATE at N > 1 (one- and four-wave helper kernels, the plain kernel above
+    RR_HELP_MAX_N; auto-reset, TimeLimit): the same stepping as a device-state batch, bitwise,
+    and the host views equal rr_get_state."""
     import torch
 
     from rl_rocket_amd.batch import RocketBatch
