@@ -291,18 +291,30 @@ class RocketBatch:
     def fetch_done(self, capacity=None):
         """Done list of the last step on the host: (idx, terminal_obs, episode_return, episode_len),
         fresh arrays of the done rows. Synchronises the stream. The rows land in persistent pinned
-        buffers (rr_host_alloc, allocated on the first call: the copies go straight to them instead
-        of through the runtime's staging of pageable memory) and are copied out."""
+        buffers (rr_host_alloc: the copies go straight to them instead of through the runtime's
+        staging of pageable memory), sized to the largest done list seen (at least 4096 rows; a
+        longer list grows them and is fetched again), and are copied out."""
         cap = self.num_envs if capacity is None else min(int(capacity), self.num_envs)
-        if getattr(self, "_fetch", None) is None:
-            n, ns = self.num_envs, self.state_dim
-            self._fetch = (HostArray((n,), np.int32), HostArray((n, ns), np.float32), HostArray((n,), np.float32),
-                           HostArray((n,), np.int32))
-        bufs = self._fetch
-        c = self.lib.rr_fetch_done(self._h, cap, *(b.ptr for b in bufs), self._stream())
-        _lib.check(c, "rr_fetch_done")
+        rows = min(cap, max(4096, len(self._fetch[0].array) if getattr(self, "_fetch", None) else 0))
+        while True:
+            if getattr(self, "_fetch", None) is None or len(self._fetch[0].array) < rows:
+                self._free_fetch()  # grown on demand (~1 % of the envs finish per step): not N rows up front
+                ns = self.state_dim
+                self._fetch = (HostArray((rows,), np.int32), HostArray((rows, ns), np.float32),
+                               HostArray((rows,), np.float32), HostArray((rows,), np.int32))
+            bufs = self._fetch
+            c = self.lib.rr_fetch_done(self._h, min(cap, rows), *(b.ptr for b in bufs), self._stream())
+            _lib.check(c, "rr_fetch_done")
+            if int(c) <= rows or rows >= cap:
+                break
+            rows = min(cap, 1 << (int(c) - 1).bit_length())  # more done envs than rows: grow, fetch again
         m = min(int(c), cap)
         return tuple(b.array[:m].copy() for b in bufs)
+
+    def _free_fetch(self):
+        for b in getattr(self, "_fetch", None) or ():
+            b.free()
+        self._fetch = None
 
     def copy_terminal(self, out=None):
         """Device copies of the terminal rows of the envs done at the last step (rr_copy_terminal:
@@ -323,9 +335,7 @@ class RocketBatch:
             self.torch.cuda.synchronize(self.device)
             self.lib.rr_destroy(self._h)
             self._h = ctypes.c_void_p()
-        for b in getattr(self, "_fetch", None) or ():
-            b.free()
-        self._fetch = None
+        self._free_fetch()
 
     def __del__(self):
         try:
