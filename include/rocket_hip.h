@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 9
+#define RR_ABI_VERSION 10
 
 /* error codes */
 #define RR_OK 0
@@ -221,6 +221,17 @@ int rr_host_free(void* p);
  * Returns the number of done envs (>= 0) or an RR_E* code. */
 int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs, float* term_return,
                       int32_t* term_len, void* stream);
+
+/* rr_fetch_done for caller-owned per-step snapshots (SB3 infos of a device-output vec env, built
+ * after later steps have run): the env indices where done[i] != 0 ([N] u8, device), ascending,
+ * and their rows of the given sources — term_obs_src [N][state_dim] f32, term_return_src [N] f32,
+ * term_len_src [N] i32, truncated_src [N] u8 (device; e.g. the rows rr_copy_terminal wrote) — into
+ * the host arrays idx / term_obs / term_return / term_len / truncated (at most `capacity` rows,
+ * any may be NULL; an output needs its source). SYNCHRONISES `stream`. Returns the number of done
+ * envs or an RR_E* code. */
+int64_t rr_gather_rows(rr_env* e, const uint8_t* done, const float* term_obs_src, const float* term_return_src,
+                       const int32_t* term_len_src, const uint8_t* truncated_src, int64_t capacity, int32_t* idx,
+                       float* term_obs, float* term_return, int32_t* term_len, uint8_t* truncated, void* stream);
 
 /* Device-to-device copy of the terminal rows of the envs done at the last step (their final
  * obs row [state_dim], episode return, episode length) into the same rows of the caller's

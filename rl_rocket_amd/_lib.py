@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
@@ -108,6 +108,7 @@ SIGNATURES = {
     "rr_host_free": (ctypes.c_int, [_P]),
     "rr_fetch_done": (ctypes.c_int64, [_P, ctypes.c_int64, _P, _P, _P, _P, _P]),
     "rr_copy_terminal": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "rr_gather_rows": (ctypes.c_int64, [_P, _P, _P, _P, _P, _P, ctypes.c_int64, _P, _P, _P, _P, _P, _P]),
     "rr_policy_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     "rr_policy_pack": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P]),
     "rr_policy_act": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, _P,

@@ -1256,8 +1256,9 @@ __global__ __launch_bounds__(kBlock) void clear_elapsed_kernel(uint32_t* counter
 // Compact the terminal rows of the (sorted) done list for one host copy.
 __global__ __launch_bounds__(kBlock) void gather_done_kernel(const int32_t* idx, int64_t count, int ns,
                                                              const float* term_obs, const float* term_ret,
-                                                             const int32_t* term_len, float* g_obs, float* g_ret,
-                                                             int32_t* g_len)
+                                                             const int32_t* term_len, const uint8_t* trunc,
+                                                             float* g_obs, float* g_ret, int32_t* g_len,
+                                                             uint8_t* g_trunc)
 {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
@@ -1265,6 +1266,7 @@ __global__ __launch_bounds__(kBlock) void gather_done_kernel(const int32_t* idx,
     for (int j = 0; j < ns; ++j) g_obs[k * ns + j] = term_obs[i * ns + j];
     g_ret[k] = term_ret[i];
     g_len[k] = term_len[i];
+    if (trunc) g_trunc[k] = trunc[i];
 }
 
 // rr_copy_terminal: the terminal rows of the envs done at the last step (done_bits) into
@@ -1502,6 +1504,7 @@ struct rr_env {
     float* g_obs;
     float* g_ret;
     int32_t* g_len;
+    uint8_t* g_trunc;   // rr_gather_rows scratch
 };
 
 namespace {
@@ -1587,6 +1590,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         {(void**)&e->term_ret, sizeof(float) * n},        {(void**)&e->term_len, sizeof(int32_t) * n},
         {(void**)&e->g_idx, sizeof(int32_t) * n},         {(void**)&e->g_obs, sizeof(float) * e->ns * n},
         {(void**)&e->g_ret, sizeof(float) * n},           {(void**)&e->g_len, sizeof(int32_t) * n},
+        {(void**)&e->g_trunc, sizeof(uint8_t) * n},
     };
     const bool exact = p->integrator == RR_INT_DOPRI5;
     e->host_state = (p->flags & RR_FLAG_HOST_STATE) != 0;
@@ -1658,7 +1662,8 @@ int rr_destroy(rr_env* e)
         e->state = nullptr;
     }
     void* ptrs[] = {e->state, e->state64, e->d_kp, e->d_xp, e->done_bits,
-                    e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len};
+                    e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len,
+                    e->g_trunc};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     delete e;
@@ -1963,6 +1968,44 @@ int rr_host_free(void* p)
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_host_free");
 }
 
+}  // extern "C"
+
+namespace {
+// The rows of the env indices `hidx` (ascending) from the given [N][ns] / [N] sources into the
+// caller's host arrays (at most `capacity` rows): one index upload, one gather kernel into the
+// env's scratch, the copies, one synchronise. Returns the number of indices or an RR_E* code.
+int64_t fetch_rows(rr_env* e, const std::vector<int32_t>& hidx, int64_t capacity, const float* src_obs,
+                   const float* src_ret, const int32_t* src_len, const uint8_t* src_trunc, int32_t* idx,
+                   float* term_obs, float* term_return, int32_t* term_len, uint8_t* trunc_out, hipStream_t s,
+                   const char* what)
+{
+    const int64_t count = (int64_t)hidx.size();
+    const int64_t m = std::min<int64_t>(count, capacity);
+    if (m == 0) return count;
+    if (idx) std::memcpy(idx, hidx.data(), sizeof(int32_t) * m);
+    if (term_obs || term_return || term_len || trunc_out) {
+        hipError_t err = hipMemcpyAsync(e->g_idx, hidx.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, s);
+        if (err != hipSuccess) return hip_fail(err, what);
+        hipLaunchKernelGGL(gather_done_kernel, dim3(grid_of(m)), dim3(kBlock), 0, s, e->g_idx, m, e->ns, src_obs,
+                           src_ret, src_len, trunc_out ? src_trunc : nullptr, e->g_obs, e->g_ret, e->g_len, e->g_trunc);
+        err = hipGetLastError();
+        if (err == hipSuccess && term_obs)
+            err = hipMemcpyAsync(term_obs, e->g_obs, sizeof(float) * e->ns * m, hipMemcpyDefault, s);
+        if (err == hipSuccess && term_return)
+            err = hipMemcpyAsync(term_return, e->g_ret, sizeof(float) * m, hipMemcpyDefault, s);
+        if (err == hipSuccess && term_len)
+            err = hipMemcpyAsync(term_len, e->g_len, sizeof(int32_t) * m, hipMemcpyDefault, s);
+        if (err == hipSuccess && trunc_out)
+            err = hipMemcpyAsync(trunc_out, e->g_trunc, sizeof(uint8_t) * m, hipMemcpyDefault, s);
+        if (err == hipSuccess) err = hipStreamSynchronize(s);
+        if (err != hipSuccess) return hip_fail(err, what);
+    }
+    return count;
+}
+}  // namespace
+
+extern "C" {
+
 int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs, float* term_return,
                       int32_t* term_len, void* stream)
 {
@@ -1984,26 +2027,34 @@ int64_t rr_fetch_done(rr_env* e, int64_t capacity, int32_t* idx, float* term_obs
             m &= m - 1;
         }
     }
-    const int64_t count = (int64_t)hidx.size();
-    const int64_t m = std::min<int64_t>(count, capacity);
-    if (m == 0) return count;
-    if (idx) std::memcpy(idx, hidx.data(), sizeof(int32_t) * m);
-    if (term_obs || term_return || term_len) {
-        err = hipMemcpyAsync(e->g_idx, hidx.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, s);
-        if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: idx upload");
-        hipLaunchKernelGGL(gather_done_kernel, dim3(grid_of(m)), dim3(kBlock), 0, s, e->g_idx, m, e->ns,
-                           e->term_obs, e->term_ret, e->term_len, e->g_obs, e->g_ret, e->g_len);
-        err = hipGetLastError();
-        if (err == hipSuccess && term_obs)
-            err = hipMemcpyAsync(term_obs, e->g_obs, sizeof(float) * e->ns * m, hipMemcpyDeviceToHost, s);
-        if (err == hipSuccess && term_return)
-            err = hipMemcpyAsync(term_return, e->g_ret, sizeof(float) * m, hipMemcpyDeviceToHost, s);
-        if (err == hipSuccess && term_len)
-            err = hipMemcpyAsync(term_len, e->g_len, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s);
-        if (err == hipSuccess) err = hipStreamSynchronize(s);
-        if (err != hipSuccess) return hip_fail(err, "rr_fetch_done: gather");
+    return fetch_rows(e, hidx, capacity, e->term_obs, e->term_ret, e->term_len, nullptr, idx, term_obs, term_return,
+                      term_len, nullptr, s, "rr_fetch_done: gather");
+}
+
+int64_t rr_gather_rows(rr_env* e, const uint8_t* done, const float* term_obs_src, const float* term_return_src,
+                       const int32_t* term_len_src, const uint8_t* truncated_src, int64_t capacity, int32_t* idx,
+                       float* term_obs, float* term_return, int32_t* term_len, uint8_t* truncated, void* stream)
+{
+    if (!e || !done) return fail(RR_EINVAL, "rr_gather_rows: null handle or done flags");
+    if (capacity < 0) return fail(RR_EINVAL, "rr_gather_rows: negative capacity");
+    if ((term_obs && !term_obs_src) || (term_return && !term_return_src) || (term_len && !term_len_src) ||
+        (truncated && !truncated_src))
+        return fail(RR_EINVAL, "rr_gather_rows: an output without its source");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t n = e->n;
+    std::vector<uint64_t> flags((n + 7) / 8, 0);  // the u8 flags, read 8 at a time
+    hipError_t err = hipMemcpyAsync(flags.data(), done, (size_t)n, hipMemcpyDefault, s);
+    if (err == hipSuccess) err = hipStreamSynchronize(s);
+    if (err != hipSuccess) return hip_fail(err, "rr_gather_rows: done flags");
+    std::vector<int32_t> hidx;
+    const uint8_t* f8 = reinterpret_cast<const uint8_t*>(flags.data());
+    for (int64_t w = 0; w < (int64_t)flags.size(); ++w) {
+        if (!flags[w]) continue;  // ~1 % of the envs finish per step: most words are zero
+        for (int64_t i = 8 * w; i < std::min<int64_t>(8 * w + 8, n); ++i)
+            if (f8[i]) hidx.push_back((int32_t)i);
     }
-    return count;
+    return fetch_rows(e, hidx, capacity, term_obs_src, term_return_src, term_len_src, truncated_src, idx, term_obs,
+                      term_return, term_len, truncated, s, "rr_gather_rows: gather");
 }
 
 int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* term_len, void* stream)

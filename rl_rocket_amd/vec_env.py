@@ -28,6 +28,7 @@ from collections.abc import Sequence
 
 import numpy as np
 
+from . import _lib
 from .batch import RocketBatch
 from .gym_compat import Box
 from .params import MAX_EPISODE_STEPS, parse_model
@@ -277,37 +278,33 @@ class RocketVecEnv(_VecEnvBase):
             })
         self._slot = 0
         self._pending = []  # unbuilt _DeviceInfos in step order
-        pin = dict(pin_memory=True)
-        self._gbuf = {"done": t.empty((n,), dtype=t.uint8, **pin), "idx_h": t.empty((n,), dtype=t.int64, **pin),
-                      "idx_d": t.empty((n,), dtype=t.int64, device=dev)}
-        for key, shape, dt in (("obs", (n, ns), t.float32), ("ret", (n,), t.float32), ("len", (n,), t.int32),
-                               ("trunc", (n,), t.uint8)):
-            self._gbuf[key + "_d"] = t.empty(shape, dtype=dt, device=dev)
-            self._gbuf[key + "_h"] = t.empty(shape, dtype=dt, **pin)
+        self._gbuf = {}  # pinned host rows of _gather_done, allocated at its first use
 
     def _gather_done(self, done, trunc, term, stamp):
-        """The done envs of a device-output step as host arrays, through preallocated device /
-        pinned buffers (no allocation per step): done flags D2H, the done rows gathered on the
-        device (index_select into fixed buffers), one copy of each to the host, one sync."""
-        t = self.batch.torch
+        """The done envs of a device-output step as host arrays: ONE library call (rr_gather_rows)
+        reads that step's done flags, gathers the done rows of its snapshot (terminal obs, return,
+        length, truncated) on the device into pinned host buffers and synchronises once."""
+        import ctypes
+
+        from .batch import HostArray
+
+        n, ns = self.num_envs, self.batch.state_dim
         g = self._gbuf
-        g["done"].copy_(done)
-        idx = np.flatnonzero(g["done"].numpy())
-        m = len(idx)
+        if g.get("rows") is None:
+            g["rows"] = (HostArray((n,), np.int32), HostArray((n, ns), np.float32), HostArray((n,), np.float32),
+                         HostArray((n,), np.int32), HostArray((n,), np.uint8))
+        h = g["rows"]
+        P = ctypes.c_void_p
+        tobs, ret, ln = term
+        c = self.batch.lib.rr_gather_rows(
+            self.batch._h, P(done.data_ptr()), P(tobs.data_ptr()), P(ret.data_ptr()), P(ln.data_ptr()),
+            P(trunc.data_ptr()), n, *(b.ptr for b in h), self.batch._stream())
+        _lib.check(c, "rr_gather_rows")
+        m = int(c)
         if not m:
             return None
-        g["idx_h"][:m].copy_(t.from_numpy(idx))
-        ii = g["idx_d"][:m]
-        ii.copy_(g["idx_h"][:m], non_blocking=True)
-        outs = []
-        for src, key in zip(tuple(term) + (trunc,), ("obs", "ret", "len", "trunc")):
-            dev, host = g[key + "_d"][:m], g[key + "_h"][:m]
-            t.index_select(src, 0, ii, out=dev)
-            host.copy_(dev, non_blocking=True)
-            outs.append(host)
-        t.cuda.current_stream(self.batch.device).synchronize()
-        tobs, ret, ln, tr = (h.numpy().copy() for h in outs)  # the pinned buffers are reused next step
-        return self._done_rows(idx, tobs, ret, ln, tr, stamp)
+        idx, tobs_h, ret_h, ln_h, tr_h = (b.array[:m].copy() for b in h)  # the pinned buffers are reused
+        return self._done_rows(idx, tobs_h, ret_h, ln_h, tr_h, stamp)
 
     def _flush_all(self):
         while self._pending:
@@ -345,6 +342,9 @@ class RocketVecEnv(_VecEnvBase):
         if self.device_outputs and getattr(self, "_pending", None):
             self._flush_all()
         self.batch.close()
+        for b in (getattr(self, "_gbuf", None) or {}).get("rows") or ():
+            b.free()
+
     def seed(self, seed=None):
         if seed is None:
             seed = int(np.random.randint(0, 2 ** 31 - 1))
