@@ -215,16 +215,11 @@ class RocketVecEnv(_VecEnvBase):
             t1 = time.perf_counter()
             self.batch.torch.cuda.synchronize(self.batch.device)
             t2 = time.perf_counter()
-        # the three small outputs as asynchronous copies into persistent pinned buffers, then the
-        # observation's blocking copy (which synchronises the stream behind them): one host round
-        # trip instead of four
-        pin = self._pinned()
-        for dst, src in zip(pin, (rew, done, trunc)):
-            dst.copy_(src, non_blocking=True)
-        obs_h = obs.cpu().numpy()
-        rew_h = pin[0].numpy().copy()
-        done_h = pin[1].numpy().astype(bool)
-        trunc_h = pin[2].numpy().copy()
+        # obs / reward / done / truncated as DMA copies into ONE fresh pinned block (PyTorch's
+        # caching host allocator: after warm-up no pinning or page faults) and one synchronise;
+        # the numpy arrays are views that keep the block alive, so every step's arrays are its own
+        # (SB3 keeps _last_obs across the next step) and nothing is copied twice on the host
+        obs_h, rew_h, done_h, trunc_h = self._to_host(obs, rew, done, trunc)
         if tm is not None:
             t3 = time.perf_counter()
         rows = None
@@ -243,13 +238,19 @@ class RocketVecEnv(_VecEnvBase):
         self.step_async(actions)
         return self.step_wait()
 
-    def _pinned(self):
-        """Persistent pinned host buffers for reward, done and truncated (host outputs)."""
-        if getattr(self, "_pin", None) is None:
-            t, n = self.batch.torch, self.num_envs
-            self._pin = (t.empty((n,), dtype=t.float32, pin_memory=True), t.empty((n,), dtype=t.uint8, pin_memory=True),
-                         t.empty((n,), dtype=t.uint8, pin_memory=True))
-        return self._pin
+    def _to_host(self, obs, rew, done, trunc):
+        """The four step outputs as numpy views of one fresh pinned block (obs [N][ns] f32,
+        reward [N] f32, done [N] bool, truncated [N] u8), after one stream synchronise."""
+        t, n, ns = self.batch.torch, self.num_envs, self.batch.state_dim
+        o_b, r_b = 4 * n * ns, 4 * n
+        blk = t.empty((o_b + r_b + 2 * n,), dtype=t.uint8, pin_memory=True)
+        views = (blk[:o_b].view(t.float32).view(n, ns), blk[o_b:o_b + r_b].view(t.float32),
+                 blk[o_b + r_b:o_b + r_b + n], blk[o_b + r_b + n:])
+        for dst, src in zip(views, (obs, rew, done, trunc)):
+            dst.copy_(src, non_blocking=True)
+        t.cuda.current_stream(self.batch.device).synchronize()
+        o, r, d, tr = (v.numpy() for v in views)
+        return o, r, d.view(np.bool_), tr  # the kernel writes done as 0 / 1
 
     def _now(self):
         return round(time.time() - self._t_start, 6)
