@@ -303,6 +303,28 @@ def timed_region(args, env, pool, dev, dist, backend, launch, gather=None):
 # ---------------------------------------------------------------------------------------------
 # rollout mode (BASELINE configs[4])
 # ---------------------------------------------------------------------------------------------
+# dense MFMA peaks, /opt/skills/guides/MI355X_MICROARCH.md: fp32 (v_mfma_f32_32x32x2_f32) 157.3
+# TF; fp16 / bf16 ~2.5 PF (fp16x3 runs three fp16 MFMAs per product: priced at the fp16 peak)
+ROLLOUT_PEAK_TFLOPS = {"fp32": 157.3, "fp16x3": 2500.0, "bf16": 2500.0}
+HIDDEN = 64  # MlpPolicy net_arch [64, 64] (SB3 1.6 default for PPO)
+
+
+def rollout_flops_per_env_step(ns, na):
+    """Algorithmic FLOPs of the policy per env-step: the pi tower + action head and the vf tower
+    + value head GEMMs of SB3's MlpPolicy (2 FLOP per multiply-add; tanh / sampling / the env
+    step's VALU work not counted)."""
+    tower = ns * HIDDEN + HIDDEN * HIDDEN
+    return 2 * (tower + HIDDEN * na) + 2 * (tower + HIDDEN)
+
+
+def rollout_bytes_per_env_step(ns, na, T):
+    """Algorithmic HBM bytes per env-step of one collect: the rollout buffer slices written per step
+    (obs, action, value, log-prob, start, reward, advantage, return) + per env and collect the
+    state planes, v0 and counter read and written once, the last value / done / start and the last
+    step's env outputs (obs, reward, done, truncated), spread over the T steps."""
+    per_step = 4 * (ns + na + 6)
+    per_collect = 2 * 4 * (ns + 2) + 3 * 4 + 4 * ns + 4 + 2
+    return per_step + per_collect / T
 def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
     """BASELINE configs[4]: N envs driving an on-device PPO rollout; the whole collect()
     (n_steps x [policy forward, Gaussian sample, env step, timeout bootstrap, buffer
@@ -402,7 +424,36 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
                          "of graphed minibatch updates (SB3 1.6 defaults: n_epochs 10), batch_size N, loss + "
                          "backward by rr_ppo_grad"}
     env.close()
+    # roofline of the collect kernel (rollout_step_kernel<..., MULTI = true>): the policy towers
+    # are the contraction (fp32 MFMA in the default precision), so the bound is the MFMA peak;
+    # algorithmic FLOPs = the two MlpPolicy towers' GEMMs (2 per multiply-add), algorithmic bytes =
+    # the rollout buffer writes + the env state loaded / stored once per collect
+    ns, na = env.state_dim, env.action_dim
+    T = args.rollout_steps
+    collect_s = e0.elapsed_time(e1) / reps * 1e-3
+    flop = rollout_flops_per_env_step(ns, na) * n * T
+    byt = rollout_bytes_per_env_step(ns, na, T) * n * T
+    peak = ROLLOUT_PEAK_TFLOPS[args.policy_dtype]
+    roof = {"bound": "mfma", "unit": "TFLOP/s", "peak": peak,
+            "flops_per_env_step": rollout_flops_per_env_step(ns, na), "flops_per_launch": flop,
+            "achieved_events": flop / collect_s / 1e12, "frac_events": flop / collect_s / 1e12 / peak,
+            "hbm": {"bytes_per_env_step": rollout_bytes_per_env_step(ns, na, T), "bytes_per_launch": byt,
+                    "achieved_GBs": byt / collect_s / 1e9, "frac": byt / collect_s / 1e9 / HBM_PEAK_GBS},
+            "timing": "events: HIP events around the replays of the one-collect hipGraph (collect kernel + policy "
+                      "pack + iteration counter); rocprof: the collect kernel's committed rocprofv3 kernel-trace mean "
+                      "(same machine code)"}
+    rp, rp_src = (None, "multi-rank run: committed 1-GPU traces are not quoted") if world > 1 else \
+        stored_rollout_rocprof(model, n, T, args.policy_dtype)
+    if rp is not None and not args.rollout_torch and ro.one_launch and not ro.per_step:
+        roof.update(achieved=flop / (rp["mean_ns"] * 1e-9) / 1e12, rocprof_mean_us=rp["mean_ns"] / 1e3,
+                    rocprof_source=rp_src)
+        roof["frac"] = roof["achieved"] / peak
+        roof["frac_source"] = "rocprof"
+    else:
+        roof.update(achieved=roof["achieved_events"], frac=roof["frac_events"], frac_source="events",
+                    rocprof_source=rp_src)
     return {
+        "roofline": roof,
         "metric": "env-steps/sec of on-device PPO rollout collection (%s, N=%d per GPU)"
                   % ("6DOF" if model == 6 else "3DOF", n),
         "value": n * world * steps / dt, "unit": "env-steps/s", "n_gpus": world, "steps": steps, "warmup": 3 * args.rollout_steps,
@@ -426,12 +477,34 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
 # ---------------------------------------------------------------------------------------------
 # CPU baselines (rank 0, N = 1)
 # ---------------------------------------------------------------------------------------------
+def _cgroup_cpus():
+    """CPUs of this process's cgroup quota (cpu.max "quota period"), or None when unlimited."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+        except (OSError, ValueError):
+            continue
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+    return None
+
+
 def host_cores():
-    """CPU threads this process may use (the GPU box shows the whole machine in
-    os.cpu_count(); its share is the affinity mask / OMP_NUM_THREADS)."""
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    """(threads the CPU legs use, how that count was found): the affinity mask, narrowed by
+    the cgroup CPU quota and OMP_NUM_THREADS when they are set (the GPU box shows the whole
+    machine in its affinity mask; its share is the quota / OMP_NUM_THREADS)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    src = {"affinity": aff}
+    n = aff
+    quota = _cgroup_cpus()
+    if quota is not None:
+        src["cgroup_quota"] = quota
+        n = min(n, quota)
     omp = os.environ.get("OMP_NUM_THREADS")
-    return max(1, min(n, int(omp))) if omp and omp.isdigit() else max(1, min(n, 16))
+    if omp and omp.isdigit() and int(omp) > 0:
+        src["OMP_NUM_THREADS"] = int(omp)
+        n = min(n, int(omp))
+    return max(1, n), src
 
 
 def cpu_baseline(model, seconds, seed=0, nthreads=1, n=1024):
@@ -492,17 +565,41 @@ def cpu_baseline(model, seconds, seed=0, nthreads=1, n=1024):
             "sample": what + ", %d thread(s), oracle/librocket_oracle.so (scipy RK45 + brentq restated in C)" % nthreads}
 
 
+def python_baseline(model, seconds):
+    """the reference algorithm in the reference's language on ONE core — ONE
+    env stepped from a Python loop by oracle/py_step.py (this repo's NumPy/SciPy restatement:
+    a Python RHS under scipy.integrate.solve_ivp RK45 with the terminal ground event, then the
+    reward, done and obs in NumPy; pinned to the reference's rows, tests/test_py_step.py)."""
+    from oracle.py_step import run_episodes
+
+    steps, busy = run_episodes(model, seconds)
+    name = "6DOF" if model == 6 else "3DOF"
+    return {"value": steps / busy, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": "%d env-steps of ONE %s env from a Python loop, oracle/py_step.py (NumPy/SciPy restatement of "
+                      "the reference's step(): solve_ivp RK45 + event, reward, done, obs; rocket_env.py:%d), %s ICs, "
+                      "U(-1,1) actions, reset on done / TimeLimit 800, 1 thread"
+                      % (steps, name, 690 if model == 6 else 150, "env_config" if model == 6 else "ctor-default")}
+
+
 def cpu_baselines(model, seconds, cores):
-    """cpu_baseline block of the bench line: the single-env leg (the north star's 'reference
-    single-env CPU step()'), the batched port on 1 core and on all host cores, the 3DOF single
-    env of configs[0], and the reference's own Python step() rates measured in the survey
-    container (it cannot run on the GPU box)."""
-    head = cpu_baseline(model, seconds * 0.35, n=1)
-    head["batched_1core"] = cpu_baseline(model, seconds * 0.25)
-    if cores > 1:
-        head["all_cores"] = cpu_baseline(model, seconds * 0.2, nthreads=cores, n=8192)
+    """cpu_baseline block of the bench line. Head: the north star's 'reference single-env CPU
+    step()' — the NumPy/SciPy single-env restatement on one core (python_restatement_1core),
+    then the C port of the same algorithm (one env per call from Python, batched on 1 core,
+    batched on every host core of the box's share), the 3DOF single env of configs[0] in both
+    forms, and the reference's own Python step() rates measured in the survey container (it
+    cannot run on the GPU box)."""
+    n_cores, src = cores
+    py6 = python_baseline(model, seconds * 0.3)
+    head = dict(py6)
+    head["python_restatement_1core"] = py6
+    head["c_port_single_env_1core"] = cpu_baseline(model, seconds * 0.15, n=1)
+    head["batched_1core"] = cpu_baseline(model, seconds * 0.15)
+    if n_cores > 1:
+        head["all_cores"] = cpu_baseline(model, seconds * 0.15, nthreads=n_cores, n=8192)
+        head["all_cores"]["cores_from"] = src
     if model == 6:
-        head["configs0_3dof_single_env"] = cpu_baseline(3, seconds * 0.2, n=1)
+        head["configs0_3dof_python_restatement_1core"] = python_baseline(3, seconds * 0.1)
+        head["configs0_3dof_single_env"] = cpu_baseline(3, seconds * 0.1, n=1)
     head["reference_python_step_survey"] = dict(REFERENCE_PY_STEP, unit="env-steps/s", cores=1,
                                                 source="reference Rocket6DOF / Rocket step(), measured in the survey "
                                                        "container (SURVEY.md §6, BASELINE.md), not on this box")
@@ -539,6 +636,73 @@ def _host_delta(a, b, dt):
     return {"process_cpu_per_wall": round((b[0] - a[0]) / dt, 3),
             "cgroup_throttled_ms": None if a[1] is None or b[1] is None else round((b[1] - a[1]) / 1e3, 1),
             "threads": b[2]}
+
+
+def sb3_collect_loop(dev, n, steps, rng):
+    """Per step, what SB3 1.6 OnPolicyAlgorithm.collect_rollouts does with a VecEnv's outputs
+    (the path main_6DOF.py:90-93's model.learn drives): np.clip of the policy's actions to the
+    action space, env.step, _update_info_buffer (info.get("episode") / info.get("is_success")
+    over every env's info) and the loop over every done flag that reads terminal_observation /
+    TimeLimit.truncated. Wall clock; the split is measured in the same pass."""
+    import collections
+
+    import numpy as np
+    import torch
+
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF, MAX_EPISODE_STEPS
+    from rl_rocket_amd.vec_env import RocketVecEnv
+
+    venv = RocketVecEnv(n, model="6DOF", device=dev, max_episode_steps=MAX_EPISODE_STEPS, monitor=True,
+                        **ENV_CONFIG_6DOF)
+    venv.reset()
+    low, high = venv.action_space.low, venv.action_space.high
+    pool = [rng.normal(0.0, 1.0, (n, 3)).astype(np.float32) for _ in range(POOL)]  # Gaussian policy samples
+    ep_info_buffer = collections.deque(maxlen=100)
+    ep_success_buffer = collections.deque(maxlen=100)
+    split = {"clip": 0.0, "step": 0.0, "update_info_buffer": 0.0, "dones_loop": 0.0}
+
+    def one(k, tm):
+        t0 = time.perf_counter()
+        clipped = np.clip(pool[k % POOL], low, high)
+        t1 = time.perf_counter()
+        _, _, dones, infos = venv.step(clipped)
+        t2 = time.perf_counter()
+        for idx, info in enumerate(infos):  # BaseAlgorithm._update_info_buffer
+            maybe_ep_info = info.get("episode")
+            maybe_is_success = info.get("is_success")
+            if maybe_ep_info is not None:
+                ep_info_buffer.extend([maybe_ep_info])
+            if maybe_is_success is not None and dones[idx]:
+                ep_success_buffer.append(maybe_is_success)
+        t3 = time.perf_counter()
+        n_boot = 0
+        for idx, done in enumerate(dones):  # the timeout bootstrap's scan
+            if done and infos[idx].get("terminal_observation") is not None and \
+                    infos[idx].get("TimeLimit.truncated", False):
+                n_boot += 1
+        t4 = time.perf_counter()
+        if tm:
+            split["clip"] += t1 - t0
+            split["step"] += t2 - t1
+            split["update_info_buffer"] += t3 - t2
+            split["dones_loop"] += t4 - t3
+        return n_boot
+
+    for k in range(100):  # the same warm-up as the other legs
+        one(k, False)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        one(k, True)
+    dt = time.perf_counter() - t0
+    torch.cuda.synchronize(dev)
+    venv.close()
+    return {"value": n * steps / dt, "unit": "env-steps/s", "us_per_step": dt / steps * 1e6, "n_envs": n,
+            "steps": steps, "split_us_per_step": {k: v / steps * 1e6 for k, v in split.items()},
+            "episodes_seen": len(ep_info_buffer),
+            "path": "SB3 1.6 collect_rollouts' per-step env work on RocketVecEnv(monitor=True) with numpy outputs: "
+                    "np.clip(actions) + step + _update_info_buffer over all N infos + the done-flag loop "
+                    "(terminal_observation / TimeLimit.truncated); the policy forward and the terminal-obs value "
+                    "calls excluded"}
 
 
 def sb3_legs(dev, n, steps):
@@ -594,6 +758,12 @@ def sb3_legs(dev, n, steps):
                       "kernel = remaining device time, d2h = obs / reward / done copies to numpy, infos = done list "
                       "(rr_fetch_done) + terminal_observation / TimeLimit.truncated / Monitor dicts of the done envs",
         "path": "RocketVecEnv(monitor=True).step(numpy actions) -> numpy obs/reward/done + lazy infos (SB3 VecEnv)"}
+
+    # what stock SB3 1.6 does around that step (collect_rollouts, on_policy_algorithm.py): clip the
+    # policy's actions, step, _update_info_buffer over ALL N infos, and the timeout-bootstrap loop
+    # over every done flag reading terminal_observation / TimeLimit.truncated (the policy forward
+    # and the value of the terminal obs are the policy's cost, not the env's: left out)
+    out["sb3_collect_loop"] = sb3_collect_loop(dev, n, steps, rng)
 
     # device outputs: device actions in, device tensors out (obs stay in HBM); with Monitor (every
     # step's infos built two steps later) and without (nothing leaves HBM unless read). The same
@@ -693,6 +863,24 @@ def stored_rocprof(model, n, steps):
     a --kernel-trace --stats run of this bench command, committed under profiles/), only if it
     was measured on THIS kernel's machine code; else (None, reason)."""
     return _stored("rocprof_step_k%d_n%%d.json" % steps, model, n)
+
+
+def stored_rollout_rocprof(model, n, T, dtype):
+    """The collect kernel's committed rocprofv3 kernel-trace mean (tools/rocprof_step.py on a
+    `bench.py --mode rollout` run) measured on this kernel's machine code; else (None, reason)."""
+    import glob
+
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "rocprof_rollout_n%d_t%d_%s.json" % (n, T, dtype)),
+                         recursive=True), key=os.path.getmtime)
+    isa = _isa_hashes()
+    stale = None
+    for path in reversed(hits):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]:
+            return d, os.path.relpath(path, ROOT)
+        stale = stale or os.path.relpath(path, ROOT)
+    return None, "no collect-kernel trace measured on this machine code (latest, other code: %s)" % stale
 
 
 def gather_leg_result(args, env, pool, dev, dist, backend, launch, n, world, K):
@@ -809,6 +997,20 @@ def main():
     if rp is not None:
         rocprof = {"mean_us": rp["mean_ns"] / 1e3, "frac": bytes_launch / (rp["mean_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS,
                    "calls": rp["calls"], "events_us_same_run": rp.get("events_kernel_us"), "source": rp_src}
+    # `frac` is the profile-evidenced figure where a committed rocprofv3 kernel trace of this
+    # command on this kernel's machine code exists (one GPU only: a stored 1-GPU trace does not
+    # describe the ranks of a multi-GPU run), the live HIP-event figure otherwise
+    stored_1gpu = None
+    if rocprof is not None and world > 1:
+        stored_1gpu, rocprof = rocprof, None
+    frac_events = achieved / HBM_PEAK_GBS
+    if rocprof is not None:
+        achieved_line, frac_line = bytes_launch / (rp["mean_ns"] * 1e-9) / 1e9, rocprof["frac"]
+        frac_source = "rocprof: %s (mean kernel-trace duration of this command, %d dispatches)" % (rp_src, rp["calls"])
+    else:
+        achieved_line, frac_line = achieved, frac_events
+        frac_source = "events: HIP events on the launch stream around the K launches of this run" + \
+            ("" if world == 1 else " (world %d: committed 1-GPU traces are not quoted)" % world)
     result = {
         "metric": "env-steps/sec (%s, N=%d per GPU)" % ("6DOF" if model == 6 else "3DOF", n),
         "value": value,
@@ -836,24 +1038,30 @@ def main():
                    "parallelism": "env-sharded x%d" % world,
                    "world_size": dist.get_world_size() if dist is not None else 1,
                    "backend": dist.get_backend() if dist is not None else None},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "achieved": achieved_line, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": frac_line, "frac_source": frac_source,
+                     "achieved_events": achieved, "frac_events": frac_events,
                      "frac_wall": achieved_wall / HBM_PEAK_GBS,
                      "frac_rocprof": rocprof["frac"] if rocprof else None,
-                     "rocprof": rocprof if rocprof else {"source": rp_src},
+                     "rocprof": rocprof if rocprof else (
+                         {"source": rp_src} if stored_1gpu is None else
+                         {"stored_1gpu_profile": stored_1gpu,
+                          "note": "a committed single-GPU rocprofv3 trace of this kernel; not a measurement of this "
+                                  "%d-rank run, so frac_rocprof is null and frac is the events figure" % world}),
                      "traffic": traffic, "traffic_unit": "B/launch",
                      "traffic_source": traffic_src,
                      "kernel": "step_kernel<%d,%s>" % (model, args.integrator.upper()),
                      "kernel_us": kern_ms * 1e3,
-                     "timing": "frac: HIP events on the launch stream around the K launches of the timed region" +
+                     "timing": "frac_events: HIP events on the launch stream around the K launches of the timed region" +
                                (" (recorded by tools/libbench_timed.so; the first 2 launches are queued behind a "
                                 "host-released gate kernel so the host's submission stays ahead)"
                                 if reg["use_loop"] else " (around the hipGraph replays)") +
                                (" (each step = rr_step_rows + the all_gather, so kernel_us includes the "
                                 "collective)" if gather is not None else "") +
                                "; frac_wall: the same bytes over the wall-clock ms_per_step; frac_rocprof: over the "
-                               "rocprofv3 kernel-trace mean of this command on this kernel source (committed "
-                               "under profiles/)",
+                               "rocprofv3 kernel-trace mean of this command on this kernel's machine code (committed "
+                               "under profiles/); frac = frac_rocprof where that trace exists (one GPU), else "
+                               "frac_events",
                      "bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": bytes_env},
     }

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 10
+#define RR_ABI_VERSION 11
 
 /* error codes */
 #define RR_OK 0
@@ -142,10 +142,11 @@ int rr_action_dim(const rr_env* e);
  * (the seed's four key words — splitmix64 of `seed` on the host — , gid, cw): deterministic,
  * independent of how envs are sharded over GPUs, and free of per-env RNG state in HBM. The
  * episode field has 32 - rr_counter_bits() bits (22 under the reference's TimeLimit 800), so
- * one env's keys do not repeat for 2^22 episodes. Host-only call: it synchronises the device
- * (no kernel still in flight reads the old key) and the new key applies to every launch that
- * runs after it, including replays of hipGraphs captured before it, at every N. `stream` is
- * unused (kept for ABI stability). */
+ * one env's keys do not repeat for 2^22 episodes. Stream-ordered host call: the key is written
+ * in the order of `stream` (launches queued on it before the call read the old key) and the
+ * call returns once it has landed (it synchronises `stream`, nothing else); it applies to every
+ * launch that runs after it, including replays of hipGraphs captured before it, at every N.
+ * RR_EINVAL while `stream` is being captured into a graph. */
 int rr_seed(rr_env* e, uint64_t seed, void* stream);
 /* Sample a fresh initial condition for every env where mask[i] != 0 (all when mask is
  * NULL), write the normalised obs [N][state_dim] (obs may be NULL). */
@@ -155,12 +156,14 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream);
  *   action    [N][action_dim] fp32 normalised in [-1,1] (not clipped, like the reference)
  *   obs       [N][state_dim] fp32 out (post-reset obs for done envs under AUTO_RESET)
  *   reward    [N] fp32 out
- *   done      [N] u8 out (ground event | bounds violation | TimeLimit)
+ *   done      [N] u8 out (ground event | bounds violation | non-finite state | TimeLimit)
  *   truncated [N] u8 out or NULL (TimeLimit.truncated)
  *   terms     [n_terms + 2][N] fp32 out or NULL: info["rewards_dict"] (6DOF 5 terms:
  *             velocity_tracking, thrust_penalty, eta, attitude_constraint, rew_goal;
- *             3DOF 6 terms: ..., attitude_hint, rew_goal), then two 0/1 planes:
- *             info["bounds_violation"] and the ground event (solve_ivp status 1) */
+ *             3DOF 6 terms: ..., attitude_hint, rew_goal), then two planes:
+ *             info["bounds_violation"] (0 / 1) and the solve_ivp status: 1 = ground event,
+ *             -1 = failure (a post-step state with a NaN / inf component: done, like the
+ *             reference's done = bool(status), rocket_env.py:702 / :158), 0 otherwise */
 int rr_step(rr_env* e, const float* action, float* obs, float* reward, uint8_t* done, uint8_t* truncated,
             float* terms, void* stream);
 

@@ -252,7 +252,12 @@ static int step_impl(solver* s)
     int rejected = 0;
     double y_new[NMAX], f_new[NMAX], err[NMAX];
     for (;;) {
-        if (h_abs < min_step) return 0;
+        /* scipy: `if h_abs < min_step: return False, TOO_SMALL_STEP`. A NaN h_abs (non-finite
+         * state or action) fails that test for ever and scipy's step never returns; written
+         * negated, the restatement ends it as TOO_SMALL_STEP (status -1 => done), as the
+         * kernels do (rocket_dopri5.inc solve(), rocket_hip.hip nonfinite()). Finite h_abs:
+         * identical. */
+        if (!(h_abs >= min_step)) return 0;
         double t_new = t + h_abs;
         if (t_new - s->t_bound > 0) t_new = s->t_bound;
         double h = t_new - t;

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6

@@ -107,14 +107,20 @@ class RocketBatch:
         shape = (self.action_dim, self.num_envs) if self.action_soa else (self.num_envs, self.action_dim)
         if a.size != self.num_envs * self.action_dim:
             raise ValueError("expected %d actions, got shape %s" % (self.num_envs * self.action_dim, a.shape))
-        if getattr(self, "_stage", None) is None:
-            self._stage = (t.empty(shape, dtype=t.float32, pin_memory=True),
-                           t.empty(shape, dtype=t.float32, device=self.device), t.cuda.Event())
-        pin, dev, ev = self._stage
-        ev.synchronize()  # the previous upload has left the staging buffer
+        # one (pinned, device) staging pair per stream: the device copy is only written and read in
+        # the order of its own stream, so a step still reading it on stream A cannot be overwritten
+        # by an upload issued on stream B
+        stream = t.cuda.current_stream(self.device)
+        stages = self.__dict__.setdefault("_stages", {})
+        st = stages.get(stream.cuda_stream)
+        if st is None:
+            st = stages[stream.cuda_stream] = (t.empty(shape, dtype=t.float32, pin_memory=True),
+                                               t.empty(shape, dtype=t.float32, device=self.device), t.cuda.Event())
+        pin, dev, ev = st
+        ev.synchronize()  # the previous upload has left the pinned buffer
         np.copyto(pin.numpy(), a.reshape(shape))
         dev.copy_(pin, non_blocking=True)
-        ev.record(t.cuda.current_stream(self.device))
+        ev.record(stream)
         return dev
 
     def _check_action(self, action):

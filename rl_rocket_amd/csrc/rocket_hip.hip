@@ -33,49 +33,32 @@
 
 namespace {
 
-#ifndef RR_RK4_GENERIC  // 1 = generic 14-component RK4 for 6DOF too (A/B reference)
-#define RR_RK4_GENERIC 0
-#endif
-#ifndef RR_NEWTON_ITERS  // Newton iterations of the event root (2: -1.2 %, parity margin 36x -> 3x)
-#define RR_NEWTON_ITERS 3
-#endif
+// Newton iterations of the event root (2: -1.2 % per step, but the oracle-parity margin drops
+// from 36x to 3x)
+constexpr int kNewtonIters = 3;
 // Cache-policy bits of the step kernel's buffer loads / stores (gfx950 CPol: 1 = sc0,
-// 2 = nt, 16 = sc1); 0 = default policy. RR_ST_AUX: library state planes; RR_OUT_AUX:
-// caller-owned outputs.
-#ifndef RR_LD_AUX
-#define RR_LD_AUX 0
-#endif
-#ifndef RR_ST_AUX
-#define RR_ST_AUX 0
-#endif
-#ifndef RR_ST_AUX_HELP  // state planes of the helper-wave step kernels (N <= RR_HELP_MAX_N)
-// sc1 (device-scope write-through) where the whole batch's state is a few MB: the end-of-kernel
-// release then has no dirty state lines to write back. A/B at N = 65536 (gpurun_out/q9, q10):
-// direct launches 4.13-4.26 vs 4.34-4.55 us per step, hipGraph replays K = 20 4.39-4.41 vs
-// 4.47-4.48, K = 2000 equal; at N = 524288 (plain kernel, default policy kept) it had cost
-// 10-25 %.
-#define RR_ST_AUX_HELP 16
-#endif
-#ifndef RR_OUT_AUX  // caller-owned outputs (obs, reward, done, truncated)
-// sc1 = device-scope write-through: the outputs leave L2 while the kernel runs instead of
-// in the end-of-kernel writeback (A/B at N = 65536: 5.49 -> 5.18 us; the same bit on the
-// state planes, which the next launch re-reads, is slower; nt loads +5 %).
-#define RR_OUT_AUX 16
-#endif
-#ifndef RR_STEP_ATTR  // occupancy floor of the step kernel: <= 128 VGPRs keeps 4 waves per SIMD at large N
-#define RR_STEP_ATTR __attribute__((amdgpu_waves_per_eu(4)))
-#endif
-#ifndef RR_HELP_MAX_N  // largest N stepped with helper waves (step_kernel<..., HELP = true>)
-#define RR_HELP_MAX_N 131072
-#endif
-#ifndef RR_NARROW_MAX_N  // largest N stepped with one main wave per workgroup (helper variant)
-#define RR_NARROW_MAX_N 16384
-#endif
-#ifndef RR_BLOCK
-#define RR_BLOCK 256
-#endif
+// 2 = nt, 16 = sc1); 0 = default policy. kStAux: library state planes (kernels above
+// kHelpMaxN); kOutAux: caller-owned outputs.
+constexpr int kLdAux = 0;
+constexpr int kStAux = 0;
+// state planes of the helper-wave step kernels (N <= kHelpMaxN): sc1 (device-scope write-through)
+// where the whole batch's state is a few MB, so the end-of-kernel release has no dirty state
+// lines to write back. A/B at N = 65536: direct launches 4.13-4.26 vs 4.34-4.55 us per step,
+// hipGraph replays K = 20 4.39-4.41 vs 4.47-4.48, K = 2000 equal; at N = 524288 (plain kernel,
+// default policy kept) it had cost 10-25 %.
+constexpr int kStAuxHelp = 16;
+// caller-owned outputs (obs, reward, done, truncated): sc1 = device-scope write-through, the
+// outputs leave L2 while the kernel runs instead of in the end-of-kernel writeback (A/B at
+// N = 65536: 5.49 -> 5.18 us; the same bit on the state planes, which the next launch re-reads,
+// is slower; nt loads +5 %).
+constexpr int kOutAux = 16;
+// largest N stepped with helper waves (step_kernel<..., HELP = true>); RR_HELP_MAX_N in the
+// environment overrides it at rr_create (tests select the plain kernel at small N with it)
+constexpr int64_t kHelpMaxN = 131072;
+// largest N stepped with one main wave per workgroup (helper variant)
+constexpr int64_t kNarrowMaxN = 16384;
 constexpr int kWave = 64;
-constexpr int kBlock = RR_BLOCK;  // threads per workgroup (A/B-tested: tools/ab_kernel.py)
+constexpr int kBlock = 256;  // threads per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // ---------------------------------------------------------------------------
@@ -253,23 +236,23 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint64_t bytes)
 }
 __device__ __forceinline__ float bld_f(rsrc_t r, uint32_t voff, uint32_t soff)
 {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, RR_LD_AUX));
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, kLdAux));
 }
 __device__ __forceinline__ uint32_t bld_u(rsrc_t r, uint32_t voff, uint32_t soff)
 {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, RR_LD_AUX);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, kLdAux);
 }
-template <int AUX = RR_ST_AUX>
+template <int AUX = kStAux>
 __device__ __forceinline__ void bst_f(rsrc_t r, float v, uint32_t voff, uint32_t soff)
 {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)soff, AUX);
 }
-template <int AUX = RR_ST_AUX>
+template <int AUX = kStAux>
 __device__ __forceinline__ void bst_u(rsrc_t r, uint32_t v, uint32_t voff, uint32_t soff)
 {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, AUX);
 }
-template <int AUX = RR_ST_AUX>
+template <int AUX = kStAux>
 __device__ __forceinline__ void bst_u8(rsrc_t r, uint8_t v, uint32_t voff)
 {
     __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)voff, 0, AUX);
@@ -639,12 +622,10 @@ __device__ __forceinline__ void integrate(const KParams& P, const Ctl& c, const 
 {
     constexpr int NS = Dims<MODEL>::NS;
     float k[NS], yt[NS];
-#if !RR_RK4_GENERIC
     if constexpr (MODEL == 6 && INTEG == RR_INT_RK4) {
         integrate6_rk4_pk(P, c, y0, y1, f0);
         return;
     }
-#endif
     if constexpr (INTEG == RR_INT_EULER) {
         rhs<MODEL>(P, c, y0, k);
 #pragma unroll
@@ -716,7 +697,7 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
         // inclusive. Fixed 3 iterations, branch-free (quadratic convergence from the secant
         // guess; the parity tests cover touchdowns down to |v| ~ 1 m/s).
 #pragma unroll
-        for (int it = 0; it < RR_NEWTON_ITERS; ++it) {
+        for (int it = 0; it < kNewtonIters; ++it) {
             const float H = fmaf(fmaf(fmaf(c3, s, c2), s, hv0), s, x0);
             const float dH = fmaf(fmaf(d3, s, d2), s, hv0);
             const bool same = (H > 0.0f) == pos0;
@@ -770,6 +751,23 @@ __device__ __forceinline__ void post_integrate(float* y1)
         float th = fmodf(y1[2], kTwoPi) + kTwoPi;
         y1[2] = fmodf(th, kTwoPi);
     }
+}
+
+// A post-step state with a NaN / inf component ends the episode: the analogue of solve_ivp's
+// status -1 (done = bool(status), simulator.py:236-241 -> rocket_env.py:702 / :158). scipy's RK45
+// never returns on such a state (a NaN step size passes its `h_abs < min_step` test forever);
+// the exact mode and the oracle stop it as TOO_SMALL_STEP (status -1), and here every
+// component enters a sum of y_j * 0, which is +-0 for finite y_j and NaN otherwise (no
+// overflow of finite values; 7 v_pk_fma_f32 for 6DOF). The terms plane reports status -1.
+template <int NS>
+__device__ __forceinline__ bool nonfinite(const float* y)
+{
+    f2 acc = pk_bc(0.0f);
+#pragma unroll
+    for (int j = 0; j + 1 < NS; j += 2) acc = pk_fma(f2{y[j], y[j + 1]}, pk_bc(0.0f), acc);
+    float s = acc.x + acc.y;
+    if constexpr (NS % 2) s = fmaf(y[NS - 1], 0.0f, s);
+    return !(s == 0.0f);
 }
 
 // Sample one initial condition: gym Box.sample (uniform in [low, high], float32),
@@ -915,11 +913,11 @@ __device__ __forceinline__ void store_obs_tile(float* lds, const float* o, rsrc_
         for (int q = 0; q < (NV + kWave - 1) / kWave; ++q) {
             const int k = lane + q * kWave;
             if (NV % kWave == 0 || k < NV)
-                __builtin_amdgcn_raw_buffer_store_b128(src4[k], obs_r, (int)(k * 16u), (int)sbase, RR_OUT_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(src4[k], obs_r, (int)(k * 16u), (int)sbase, kOutAux);
         }
     } else {
         const int tot = (int)nvalid * NS;
-        for (int k = lane; k < tot; k += kWave) bst_f<RR_OUT_AUX>(obs_r, lds[k], k * 4u, sbase);
+        for (int k = lane; k < tot; k += kWave) bst_f<kOutAux>(obs_r, lds[k], k * 4u, sbase);
     }
 }
 
@@ -943,12 +941,12 @@ __device__ __forceinline__ void load_action(rsrc_t act_r, uint32_t vo, uint32_t 
 #pragma unroll
         for (int j = 0; j < NA; ++j) a[j] = bld_f(act_r, vo, j * plane);
     } else if constexpr (NA == 3) {
-        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)((vo << 1) + vo), 0, RR_LD_AUX);  // 12 B rows
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(act_r, (int)((vo << 1) + vo), 0, kLdAux);  // 12 B rows
         a[0] = __uint_as_float(v.x);
         a[1] = __uint_as_float(v.y);
         a[2] = __uint_as_float(v.z);
     } else {
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(vo << 1), 0, RR_LD_AUX);  // 8 B rows
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(act_r, (int)(vo << 1), 0, kLdAux);  // 8 B rows
         a[0] = __uint_as_float(v.x);
         a[1] = __uint_as_float(v.y);
     }
@@ -1036,24 +1034,24 @@ __device__ __forceinline__ void store_terminal(const Bufs& B, uint32_t i, uint32
 // truncated, optional terms
 template <int NT, bool REWARD_DONE = true>
 __device__ __forceinline__ void store_outputs(const StepIO& io, uint32_t i, uint32_t vo, uint32_t plane, uint32_t n,
-                                              float r, bool done, bool trunc, const float* t, bool bv, bool event)
+                                              float r, bool done, bool trunc, const float* t, bool bv, float status)
 {
     if constexpr (REWARD_DONE) {
-        bst_f<RR_OUT_AUX>(make_rsrc(io.reward, plane), r, vo, 0);
-        bst_u8<RR_OUT_AUX>(make_rsrc(io.done, n), (uint8_t)done, i);
+        bst_f<kOutAux>(make_rsrc(io.reward, plane), r, vo, 0);
+        bst_u8<kOutAux>(make_rsrc(io.done, n), (uint8_t)done, i);
     }
-    if (io.truncated) bst_u8<RR_OUT_AUX>(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
+    if (io.truncated) bst_u8<kOutAux>(make_rsrc(io.truncated, n), (uint8_t)trunc, i);
     if (io.terms) {
         const rsrc_t tr = make_rsrc(io.terms, (uint64_t)(NT + 2) * plane);
 #pragma unroll
         for (int j = 0; j < NT; ++j) bst_f(tr, t[j], vo, j * plane);
         bst_f(tr, bv ? 1.0f : 0.0f, vo, NT * plane);           // info["bounds_violation"]
-        bst_f(tr, event ? 1.0f : 0.0f, vo, (NT + 1) * plane);  // solve_ivp status == 1
+        bst_f(tr, status, vo, (NT + 1) * plane);  // solve_ivp status: 1 ground event, -1 non-finite state, 0
     }
 }
 
 // The step kernel: one env per lane, 64 envs per wave.
-// HELP (N <= RR_HELP_MAX_N, about one main wave per SIMD): the auto-reset candidates of main
+// HELP (N <= kHelpMaxN, about one main wave per SIMD): the auto-reset candidates of main
 // wave k are drawn by helper wave WPB + k of the same workgroup (on the same SIMD) into
 // cand[k] (row per lane: NS values, v0), published by cflag[k]. A lone wave issues one VALU op
 // per 4 cycles and its SIMD can take one per 2 (MI355X_MICROARCH.md, 'vector-instruction ISSUE
@@ -1067,7 +1065,8 @@ __device__ __forceinline__ void store_outputs(const StepIO& io, uint32_t i, uint
 // buffer of the multi-GPU all-gather (rl_rocket_amd.dist.ShardGather).
 #ifndef RR_TU_EXACT  // rocket_exact.hip compiles this file again for the exact-mode kernels only
 template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB, bool ROWS>
-__global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR void step_kernel(
+// amdgpu_waves_per_eu(4): <= 128 VGPRs keeps 4 waves per SIMD at large N
+__global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(
     float* __restrict__ state, const float* __restrict__ action, uint32_t n_envs, uint32_t mode, const KParams P,
     const Bufs B, const StepIO io)
 {
@@ -1120,7 +1119,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     // (rr_create), so a single descriptor (4 SGPRs) serves them all via soffset
     const rsrc_t st_r = make_rsrc(state, (uint64_t)(NS + 3) * plane);
     const uint32_t v0_off = NS * plane, cw_off = (NS + 1) * plane, ret_off = (NS + 2) * plane;
-    constexpr int SA = HELP ? RR_ST_AUX_HELP : RR_ST_AUX;  // cache policy of the state-buffer stores
+    constexpr int SA = HELP ? kStAuxHelp : kStAux;  // cache policy of the state-buffer stores
 
     // ---- all loads first (one memory round trip per wave); the counter word first, so the
     // reset candidate below is drawn while the state planes are still in flight ----
@@ -1153,10 +1152,11 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
     }
 
     const bool event = physics_step<MODEL, INTEG>(P, a, y0, y1);
+    const bool nf = nonfinite<NS>(y1);
     bool bv;
     float t[NT];
     const float r = reward_terms<MODEL>(H, y1, a, v0, bv, t);
-    bool done = event || bv, trunc;
+    bool done = event || bv || nf, trunc;
     int32_t el = CL.time_limit(cw, done, trunc);
     ret += r;
     float o[NS];
@@ -1197,7 +1197,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) RR_STEP_ATTR 
         for (int j = 0; j < NS; ++j) bst_f<SA>(st_r, y1[j], vo, j * plane);
         if (use_counter) bst_u<SA>(st_r, cw, vo, (NS + 1) * plane);
         if (mode & RR_FLAG_EPISODE_STATS) bst_f<SA>(st_r, ret, vo, (NS + 2) * plane);
-        store_outputs<NT, !ROWS>(io, i, vo, plane, n, r, done, trunc, t, bv, event);
+        store_outputs<NT, !ROWS>(io, i, vo, plane, n, r, done, trunc, t, bv, event ? 1.0f : (nf ? -1.0f : 0.0f));
     }
     const uint32_t nvalid = (n - wave_base) < (uint32_t)kWave ? (n - wave_base) : (uint32_t)kWave;
     if constexpr (ROWS) {
@@ -1487,7 +1487,7 @@ struct rr_env {
     int ns, na, nt;
     int64_t n, id_off;
     uint64_t steps;
-    int64_t help_max_n;       // largest N stepped with helper waves (RR_HELP_MAX_N, env override)
+    int64_t help_max_n;       // largest N stepped with helper waves (kHelpMaxN, RR_HELP_MAX_N env override)
     float* state;
     float* v0;
     uint32_t* counter;
@@ -1577,7 +1577,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     {
         // test / A-B override of the helper-wave threshold: RR_HELP_MAX_N=<n> in the environment
         const char* hv = std::getenv("RR_HELP_MAX_N");
-        e->help_max_n = hv ? std::strtoll(hv, nullptr, 10) : (int64_t)RR_HELP_MAX_N;
+        e->help_max_n = hv ? std::strtoll(hv, nullptr, 10) : kHelpMaxN;
     }
     DeviceGuard g(device);
     struct A {
@@ -1679,15 +1679,22 @@ int rr_seed(rr_env* e, uint64_t seed, void* stream)
     // The reset stream is counter-based and every kernel reads its key from the device copy of
     // the parameters (Bufs.kp), so the new key applies to every launch that runs after this call
     // — graph replays of launches captured before it included — whatever the batch size. The
-    // device is synchronised first: no kernel still running on any stream reads the copy while
-    // it is rewritten.
-    (void)stream;
+    // copy is written in the order of `stream` (the handle's stream: every launch queued on it
+    // before this call reads the old key) and the call returns once it has landed. Refused
+    // while `stream` is being captured: the key is not a graph node (replays read the key
+    // current when they run).
     if (!e) return fail(RR_EINVAL, "rr_seed: null handle");
     DeviceGuard g(e->device);
-    hipError_t err = hipDeviceSynchronize();
-    if (err != hipSuccess) return hip_fail(err, "rr_seed: device sync");
+    hipStream_t s = (hipStream_t)stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipError_t err = hipStreamIsCapturing(s, &cs);
+    if (err != hipSuccess) return hip_fail(err, "rr_seed: hipStreamIsCapturing");
+    if (cs != hipStreamCaptureStatusNone)
+        return fail(RR_EINVAL, "rr_seed: the stream is being captured into a graph (seed before capturing: "
+                               "replays read the key current when they run)");
     seed_words(seed, e->kp.seed_w);
-    err = hipMemcpy(e->d_kp, &e->kp, sizeof(KParams), hipMemcpyHostToDevice);
+    err = hipMemcpyAsync(e->d_kp, &e->kp, sizeof(KParams), hipMemcpyHostToDevice, s);
+    if (err == hipSuccess) err = hipStreamSynchronize(s);  // e->kp is pageable host memory: wait until it is read
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_seed: params upload");
 }
 
@@ -1741,7 +1748,7 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
         const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;
         // up to 16 384 envs one main wave per workgroup (64 + 64 threads): the few workgroups
         // spread over 4x as many CUs (A/B at N = 4 096: -5 % 6DOF); above, 4 main waves
-        const bool narrow = e->n <= RR_NARROW_MAX_N;
+        const bool narrow = e->n <= kNarrowMaxN;
 #define RR_LAUNCH(M, I, A)                                                                                          \
     do {                                                                                                             \
         if (help && narrow)                                                                                          \

@@ -613,6 +613,11 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
     ``ClipAdam`` (one launch) on the optimizer's own state; the all_reduce is unchanged."""
     n = ro.n_steps * ro.env.num_envs
     if fused:
+        if n % min(batch_size, n) == 1:
+            # checked before the first minibatch: a 1-row remainder cannot be normalised (PPOGrad
+            # refuses it) and failing there would leave the epoch's earlier Adam steps applied
+            raise ValueError("n_steps * num_envs = %d leaves a 1-row last minibatch at batch_size %d (rr_ppo_grad "
+                             "needs >= 2 rows); choose another batch_size" % (n, batch_size))
         grad = PPOGrad(policy, ro, min(batch_size, n), clip_range, ent_coef, vf_coef)
         params = list(policy.parameters())
         adam = ClipAdam(optimizer, params, max_grad_norm) if clip_adam_supported(optimizer, params) else None

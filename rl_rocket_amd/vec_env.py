@@ -22,7 +22,14 @@ truncated flags and the terminal rows of THAT step's done envs, copied device to
 reading them late still describes their own step. With ``monitor=True`` infos nobody reads are
 built before their snapshot is reused, so every finished episode reaches the Monitor statistics
 in step order; without it an unread snapshot is dropped unbuilt and nothing leaves HBM.
+
+Late reads (device outputs, ``monitor=False``): the infos of step t must be read (indexed,
+iterated or ``materialize()``-d) before step t + 2 — SB3's collect_rollouts reads them at once.
+A wrapper or callback that keeps an unread infos object across two more steps gets a
+RuntimeError on its first access, where DummyVecEnv's plain list would still answer; call
+``materialize()`` on it before stepping on to keep it.
 """
+import itertools
 import time
 from collections.abc import Sequence
 
@@ -62,20 +69,37 @@ class _DoneRows:
         k = self.pos.get(i)
         if k is None:
             return None
-        d = {"terminal_observation": self.tobs[k]}
-        if self.trunc[k]:
+        return self._dict(k, self.tobs[k], bool(self.trunc[k]), float(self.ret[k]), int(self.ln[k]))
+
+    def _dict(self, k, tobs, trunc, ret, ln):
+        d = {"terminal_observation": tobs}
+        if trunc:
             d["TimeLimit.truncated"] = True
-        elif self.max_steps and self.ln[k] >= self.max_steps:
+        elif self.max_steps and ln >= self.max_steps:
             d["TimeLimit.truncated"] = False
         if self.monitor:
-            d["episode"] = {"r": round(float(self.ret[k]), 6), "l": int(self.ln[k]), "t": self.stamp}
+            d["episode"] = {"r": round(ret, 6), "l": ln, "t": self.stamp}
         return d
+
+    def items(self):
+        """(env index, info dict) of every done env, built in one pass over the arrays."""
+        tobs = list(self.tobs)  # row views
+        return [(i, self._dict(k, tobs[k], t, r, ln)) for k, (i, t, r, ln) in
+                enumerate(zip(self.idx.tolist(), self.trunc.astype(bool).tolist(), self.ret.tolist(),
+                              self.ln.tolist()))]
 
 
 class LazyInfos(Sequence):
     """SB3 ``infos`` list whose dicts are built on access: {} for running envs (plus
     ``rewards_dict`` / ``bounds_violation`` with info_terms), the done envs' dicts from their
-    arrays (``_DoneRows``)."""
+    arrays (``_DoneRows``).
+
+    Indexing builds one dict (the done envs SB3 looks at cost O(#done)); iterating — what SB3
+    1.6 ``collect_rollouts`` -> ``_update_info_buffer`` does with every step's infos — builds the
+    whole list once, in one list comprehension with the done envs' dicts spliced in, and
+    iterates that plain list (``Sequence.__iter__`` would call ``__getitem__`` N times, ~10x
+    slower at N = 65 536). Every env's dict is its own object, as in DummyVecEnv, and indexing
+    after iterating returns the same objects."""
 
     def __init__(self, n, done_rows=None, terms=None, term_names=None):
         self._n = n
@@ -83,9 +107,16 @@ class LazyInfos(Sequence):
         self._terms = terms             # host [n_terms+2, N] array or None
         self._names = term_names
         self._cache = {}
+        self._list = None               # the materialised list (first __iter__)
 
     def __len__(self):
         return self._n
+
+    def _terms_of(self, i, d):
+        t = self._terms
+        d["rewards_dict"] = {k: float(t[j, i]) for j, k in enumerate(self._names)}
+        d["bounds_violation"] = bool(t[len(self._names), i] > 0.5)
+        return d
 
     def __getitem__(self, i):
         if isinstance(i, slice):
@@ -94,17 +125,39 @@ class LazyInfos(Sequence):
             i += self._n
         if not 0 <= i < self._n:
             raise IndexError(i)
+        if self._list is not None:
+            return self._list[i]
         d = self._cache.get(i)
         if d is None:
             d = (self._rows.info(i) if self._rows is not None else None)
             if d is None:
                 d = {}
             if self._terms is not None:
-                t = self._terms
-                d["rewards_dict"] = {k: float(t[j, i]) for j, k in enumerate(self._names)}
-                d["bounds_violation"] = bool(t[len(self._names), i] > 0.5)
+                self._terms_of(i, d)
             self._cache[i] = d
         return d
+
+    def materialize(self):
+        """The infos as a plain list of N dicts (built once; dicts already handed out by
+        indexing are kept)."""
+        if self._list is None:
+            n = self._n
+            if self._terms is None:
+                lst = list(itertools.starmap(dict, itertools.repeat((), n)))  # N fresh dicts, ~25 % under a comprehension
+            else:  # info_terms: every env's dict carries its reward terms (opt-in, O(N) by nature)
+                lst = [self._terms_of(i, {}) for i in range(n)]
+            if self._rows is not None:
+                for i, d in self._rows.items():
+                    if self._terms is not None:
+                        d.update(lst[i])
+                    lst[i] = d
+            for i, d in self._cache.items():
+                lst[i] = d
+            self._list, self._cache = lst, {}
+        return self._list
+
+    def __iter__(self):
+        return iter(self.materialize())
 
     def done_indices(self):
         return [] if self._rows is None else self._rows.idx.tolist()
@@ -146,11 +199,20 @@ class _DeviceInfos(LazyInfos):
     def __len__(self):
         return self._n
 
-    def __getitem__(self, i):
+    def _live(self):
         if self._built is None and self._slot is None:
             raise RuntimeError("the infos of this step were read after their snapshot was reused (two steps "
                                "later); with monitor=False unread infos are not kept")
-        return self._build()[i]
+        return self._build()
+
+    def __getitem__(self, i):
+        return self._live()[i]
+
+    def __iter__(self):
+        return iter(self._live())
+
+    def materialize(self):
+        return self._live().materialize()
 
     def done_indices(self):
         if self._built is None and self._slot is None:
@@ -377,7 +439,12 @@ class RocketVecEnv(_VecEnvBase):
         raise AttributeError("RocketVecEnv has no per-env python objects (method %r)" % method_name)
 
     def env_is_wrapped(self, wrapper_class, indices=None):
-        return [False for _ in self._indices(indices)]
+        """True for the wrappers the fused step reproduces: SB3's ``Monitor`` (monitor=True; its
+        ``info["episode"]`` is what SB3's evaluate_policy reads when this is True) and gym's
+        ``TimeLimit`` (max_episode_steps > 0), as in main_6DOF.py:18-24's make_env."""
+        name = getattr(wrapper_class, "__name__", "")
+        wrapped = (name == "Monitor" and bool(self.monitor)) or (name == "TimeLimit" and bool(self.max_episode_steps))
+        return [wrapped for _ in self._indices(indices)]
 
     def render(self, mode="human"):
         return None

@@ -55,7 +55,8 @@ def test_golden3_single_step(golden3):
 @pytest.mark.parametrize("model", [6, 3])
 def test_golden_trajectories(model, golden6, golden3):
     """G7: 50-step fixed-action trajectories chained on the GPU (fp32 state carried
-    across steps) stay within the drift envelope of the fp64 reference."""
+    across steps) stay within the north star's 1e-5 floored-relative of the fp64 reference's
+    own trajectory at every step."""
     import torch
     from rl_rocket_amd.batch import RocketBatch
 
@@ -82,7 +83,7 @@ def test_golden_trajectories(model, golden6, golden3):
         alive &= ~done.cpu().numpy().astype(bool)
     b.close()
     print("model", model, "50-step drift", worst)
-    assert worst < 2e-4
+    assert worst < TOL_STATE  # the north star's 1e-5 after 50 chained fp32 steps (measured 2.4e-6)
 
 
 def _random_states6(n, seed=0):

@@ -387,3 +387,51 @@ def test_copy_terminal_writes_only_the_done_rows():
     rest = np.setdiff1d(np.arange(n), idx)
     assert np.isnan(tobs.cpu().numpy()[rest]).all()
     assert (ret.cpu().numpy()[rest] == -7.0).all() and (ln.cpu().numpy()[rest] == -1).all()
+
+
+def test_seed_is_stream_ordered_and_refused_inside_a_capture():
+    """rr_seed writes the key in the order of the env's stream (launches queued before
+    it on that stream read the old key; it synchronises that stream only) and refuses a stream that
+    is being captured (RR_EINVAL) instead of synchronising the device inside a capture; the
+    capture itself stays valid and replays bitwise like the eager twin."""
+    import torch
+    from rl_rocket_amd import _lib
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 4096 + 77
+    mk = lambda: RocketBatch(n, model=6, device="cuda:0", max_episode_steps=3, **_env6())  # noqa: E731
+    a, b = mk(), mk()
+    for e in (a, b):
+        e.reset()
+    acts = _actions(n, a.action_dim, 4, 5)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for k, act in enumerate(acts):
+                b.step(act)
+                if k == 1:
+                    with pytest.raises(_lib.RocketHipError, match="captured"):
+                        b.seed(99)
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    for act in acts:
+        a.step(act)
+    torch.cuda.synchronize()
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.get_state()[0], b.get_state()[0])
+    # stream order: steps queued on the stream before the re-seed keep the old key, after it the new
+    c, d = mk(), mk()
+    for e in (c, d):
+        e.reset()
+    for act in acts[:2]:
+        c.step(act)
+        d.step(act)
+    c.seed(1234)  # right behind the queued steps, no synchronise of ours in between
+    torch.cuda.synchronize()
+    d.seed(1234)
+    for act in acts[2:]:
+        c.step(act)
+        d.step(act)
+    torch.cuda.synchronize()
+    assert torch.equal(c.obs, d.obs) and torch.equal(c.get_state()[0], d.get_state()[0])

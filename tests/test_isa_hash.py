@@ -1,6 +1,6 @@
 """The evidence keys of bench.py (no GPU needed): per-kernel ISA hashes of the built library
 cover both translation units (fast kernels, exact-mode kernels), ignore where a kernel sits in
-the code object, and the committed round-3 profiles of the headline kernel match the library
+the code object, and the committed profiles of the headline kernel (profiles/r04) match the library
 this tree builds (so the bench line quotes them)."""
 import json
 import os
@@ -54,7 +54,7 @@ def test_committed_headline_evidence_matches_this_build(hashes):
     traffic, src = bench.stored_traffic(6, 65536)
     d, rsrc = bench.stored_rocprof(6, 65536, 20)
     if traffic is None or d is None:
-        pytest.fail("the committed r03 profiles do not match this build's step kernel: %s / %s" % (src, rsrc))
+        pytest.fail("the committed profiles do not match this build's step kernel: %s / %s" % (src, rsrc))
     with open(os.path.join(ROOT, src)) as f:
         rec = json.load(f)
     assert hashes[rec["kernel_name"]] == rec["isa_hash"]

@@ -1,0 +1,79 @@
+#!/bin/bash
+# One GPU session of the round (phases in one gpurun call). Every GPU step has its own timeout;
+# a crash / timeout / abort ends the script (exit codes other than 0 / 1 stop it).
+#   tools/gpu_session.sh TAG "PHASES"   PHASES: any of tests bench dist prof pmc rollout exact
+#   (default: tests bench prof pmc rollout)
+TAG=${1:-run}
+PHASES=${2:-"tests bench prof pmc rollout"}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 2
+OUT="$R/gpurun_out/$TAG"
+mkdir -p "$OUT"
+step() {  # step NAME TIMEOUT cmd...: 0 = ok, 1 = test failures (continue), anything else = stop
+  local name=$1 to=$2; shift 2
+  echo "[$name] start $(date +%T)" >&2
+  timeout -k 10 "$to" "$@"
+  local rc=$?
+  echo "[$name] exit $rc" | tee -a "$OUT/status.txt"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
+}
+has() { case " $PHASES " in *" $1 "*) return 0;; esac; return 1; }
+python -c "import rl_rocket_amd.build as b; print(b.source_hash())" > "$OUT/source_hash.txt"
+B="python $R/bench.py"
+if has tests; then
+  step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+  tail -3 "$OUT/pytest_gpu.log"
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+fi
+if has bench; then
+  # the driver's protocol, with the CPU baselines and the SB3-facing legs
+  step bench_k20_1 500 $B --steps 20 --warmup 5 > "$OUT/bench_k20_1.json" 2> "$OUT/bench_k20_1.err"
+  cat "$OUT/bench_k20_1.json"
+  step bench_k20_2 300 $B --steps 20 --warmup 5 --no-cpu-baseline --no-sb3-legs > "$OUT/bench_k20_2.json" 2> "$OUT/bench_k20_2.err"
+  step bench_k2000 300 $B --no-cpu-baseline --no-sb3-legs > "$OUT/bench_k2000.json" 2> "$OUT/bench_k2000.err"
+fi
+if has dist; then
+  (export RR_BENCH_ONE_DEVICE=1 RR_BENCH_BACKEND=gloo; step bench_gpus2_gloo 400 $B --gpus 2 --steps 20 --warmup 5 > "$OUT/bench_gpus2_gloo.json" 2> "$OUT/bench_gpus2_gloo.err") || exit $?
+  cat "$OUT/bench_gpus2_gloo.json"
+  step bench_gather_w1 300 $B --gather-leg --steps 20 --warmup 5 --no-cpu-baseline --no-sb3-legs > "$OUT/bench_gather_w1.json" 2> "$OUT/bench_gather_w1.err"
+fi
+export TMPDIR=/tmp
+if has prof; then
+  # the driver's command under rocprofv3 --kernel-trace --stats (K = 20, N = 65536 and the sweep N)
+  for N in 65536 524288; do
+    mkdir -p "$OUT/rp_k20_n$N"
+    (cd /tmp && step rp_n$N 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rp_k20_n$N" -o bench -- python "$R/bench.py" --n $N --steps 20 --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$OUT/rp_k20_n$N/bench.json" 2> "$OUT/rp_k20_n$N/bench.err") || exit $?
+    python tools/rocprof_step.py "$OUT/rp_k20_n$N" --out "$OUT/rocprof_step_k20_n$N.json" > /dev/null
+  done
+fi
+if has pmc; then
+  cd /tmp || exit 2
+  step pmc_SQ 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmc_SQ" -o pmc -- python "$R/bench.py" --no-cpu-baseline --no-sb3-legs --steps 256 --warmup 20 --n-sweep "" > "$OUT/pmc_SQ.log" 2>&1
+  step pmc_SQ2 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32 --output-format csv -d "$OUT/pmc_SQ2" -o pmc -- python "$R/bench.py" --no-cpu-baseline --no-sb3-legs --steps 256 --warmup 20 --n-sweep "" > "$OUT/pmc_SQ2.log" 2>&1
+  for C in FETCH_SIZE WRITE_SIZE; do
+    step pmc_$C 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- python "$R/bench.py" --no-cpu-baseline --no-sb3-legs --steps 256 --warmup 20 --n-sweep "" > "$OUT/pmc_$C.log" 2>&1
+  done
+  cd "$R" || exit 2
+  python tools/pmc_traffic.py "$OUT" --n 65536 --out "$OUT/pmc_traffic_n65536.json" > /dev/null
+  python tools/sq_summary.py "$OUT" --out "$OUT/sq_counters.json" > /dev/null
+fi
+if has rollout; then
+  # configs[4]: the collect rate + its roofline, the collect kernel under the tracer and its SQ counters
+  step rollout 400 $B --mode rollout --steps 320 > "$OUT/rollout.json" 2> "$OUT/rollout.err"
+  cat "$OUT/rollout.json" | head -c 600; echo
+  mkdir -p "$OUT/rp_rollout"
+  (cd /tmp && step rp_rollout 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rp_rollout" -o bench -- python "$R/bench.py" --mode rollout --steps 320 > "$OUT/rp_rollout/bench.json" 2> "$OUT/rp_rollout/bench.err") || exit $?
+  python tools/rocprof_step.py "$OUT/rp_rollout" --out "$OUT/rocprof_rollout_n65536_t16_fp32.json" > /dev/null
+  cd /tmp || exit 2
+  step rollout_SQ 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/rollout_SQ" -o pmc -- python "$R/bench.py" --mode rollout --steps 64 > "$OUT/rollout_SQ.log" 2>&1
+  cd "$R" || exit 2
+fi
+if has exact; then
+  step bench_exact 300 $B --integrator dopri5 --steps 200 --warmup 10 --no-cpu-baseline --n-sweep "" > "$OUT/bench_exact.json" 2> "$OUT/bench_exact.err"
+  cat "$OUT/bench_exact.json"
+  for N in 65536 524288; do
+    mkdir -p "$OUT/exact_kt_n$N"
+    (cd /tmp && step exact_kt_n$N 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/exact_kt_n$N" -o bench -- python "$R/bench.py" --integrator dopri5 --n $N --steps 50 --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$OUT/exact_kt_n$N/bench.json" 2>&1) || exit $?
+  done
+fi
+echo done

@@ -4,6 +4,7 @@ kernel source hash, so that bench.py can quote it beside its own HIP-event time
 
     rocprofv3 --kernel-trace --stats --output-format csv -d DIR -o bench -- python bench.py ARGS > DIR/bench.json
     python tools/rocprof_step.py DIR --out profiles/r03/<tag>/rocprof_step_k<K>_n<N>.json
+    (a bench.py --mode rollout line: --out .../rocprof_rollout_n<N>_t<T>_<dtype>.json, the collect kernel)
 
 Reads DIR/**/*kernel_stats.csv (the step_kernel row: calls, mean / min / max ns) and the bench
 line the same command printed (its HIP-event time under the profiler, N, K, bytes per launch).
@@ -34,17 +35,37 @@ def main():
     if not stats:
         raise SystemExit("no *kernel_stats.csv under %s" % a.run_dir)
     model = 6 if "6DOF" in line["metric"] else 3
+    rollout = "gpu_ms_per_collect" in line
+    pat = (r"(?<![A-Za-z_])rollout_step_kernel<%d,\d+,\d+,true," if rollout else r"(?<![A-Za-z_])step_kernel<%d,") % model
     row = None
     for path in stats:
         with open(path) as f:
             for r in csv.DictReader(f):
-                if re.search(r"(?<![A-Za-z_])step_kernel<%d," % model, r["Name"].replace(" ", "")):
+                if re.search(pat, r["Name"].replace(" ", "")):
                     if row is None or int(r["Calls"]) > int(row["Calls"]):
                         row = r
     if row is None:
-        raise SystemExit("no step_kernel<%d,...> row in %s" % (model, stats))
+        raise SystemExit("no %s row in %s" % (pat, stats))
     rf = line["roofline"]
     mean = float(row["AverageNs"])
+    if rollout:  # the collect kernel (bench.py --mode rollout): FLOPs against the MFMA peak
+        res = {
+            "kernel": "rollout_step_kernel<%d,MULTI>" % model, "kernel_name": row["Name"],
+            "isa_hash": kernel_isa_hashes().get(row["Name"]), "n": line["config"]["envs_per_gpu"],
+            "calls": int(row["Calls"]), "mean_ns": mean, "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"]),
+            "flops_per_launch": rf["flops_per_launch"], "peak_tflops": rf["peak"],
+            "achieved_tflops": rf["flops_per_launch"] / (mean * 1e-9) / 1e12,
+            "frac": rf["flops_per_launch"] / (mean * 1e-9) / 1e12 / rf["peak"],
+            "events_ms_per_collect_under_profiler": line["gpu_ms_per_collect"],
+            "method": "rocprofv3 --kernel-trace --stats of bench.py --mode rollout (all dispatches of the collect "
+                      "kernel in the process)", "source": a.run_dir, "source_hash": source_hash()}
+        text = json.dumps(res, indent=1)
+        print(text)
+        if a.out:
+            os.makedirs(os.path.dirname(a.out), exist_ok=True)
+            with open(a.out, "w") as f:
+                f.write(text + "\n")
+        return
     res = {
         "kernel": "step_kernel<%d,%s>" % (model, line["config"]["integrator"].upper()),
         "kernel_name": row["Name"],
