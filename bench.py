@@ -94,6 +94,8 @@ def parse(argv=None):
     ap.add_argument("--rollout-per-step", action="store_true",
                     help="rollout mode: one rr_rollout_step launch per step (+ bootstrap + GAE launches) instead "
                          "of the whole collect in one rr_rollout_collect launch")
+    ap.add_argument("--no-ppo", action="store_true",
+                    help="rollout mode: the collect only (no PPO update legs), e.g. for counter passes")
     ap.add_argument("--rollout-torch", action="store_true",
                     help="rollout policy / bootstrap / GAE as PyTorch ops instead of the fused HIP kernels")
     return ap.parse_args(argv)
@@ -388,11 +390,12 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
         torch.cuda.synchronize(dev)
         return time.perf_counter() - t1, out
 
-    ppo_update(pol, opt, ro, n_epochs=1, batch_size=n, group=grp)
-    upd, stats = timed(lambda: ppo_update(pol, opt, ro, n_epochs=1, batch_size=n, group=grp))
-    update = {"minibatches_per_epoch": args.rollout_steps, "batch_size": n, "eager_epoch_ms": upd * 1e3}
-    train = None
-    if dist is None or dist.get_backend() == "nccl":
+    update, stats, train = None, None, None
+    if not args.no_ppo:
+        ppo_update(pol, opt, ro, n_epochs=1, batch_size=n, group=grp)
+        upd, stats = timed(lambda: ppo_update(pol, opt, ro, n_epochs=1, batch_size=n, group=grp))
+        update = {"minibatches_per_epoch": args.rollout_steps, "batch_size": n, "eager_epoch_ms": upd * 1e3}
+    if not args.no_ppo and (dist is None or dist.get_backend() == "nccl"):
         gt = GraphedPPOUpdate(pol, opt, ro, batch_size=n, group=grp, fused=False)
         gt.update(n_epochs=1)
         gupd, _ = timed(lambda: gt.update(n_epochs=3))

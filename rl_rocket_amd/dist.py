@@ -6,7 +6,7 @@ collective is optional: reassembling the per-step outputs of all shards on every
 global batch. Ranks own envs [offset, offset + n_local); the reset stream is keyed on
 global ids, so results do not depend on the shard layout
 (tests/test_gpu_state.py::test_sharded_stepping_is_bitwise_one_batch; multi-rank:
-tools/dist_check.py under torchrun, profiles/r03/).
+tests/test_gpu_dist.py: two ranks as separate processes, bitwise one batch).
 """
 
 

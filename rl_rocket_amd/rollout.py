@@ -25,7 +25,7 @@ class _LinearFn(torch.autograd.Function):
 
     On PyTorch 2.10 / ROCm 7 a hipGraph that runs a GEMM and then a column sum (``sum(0)``) of a
     tensor produced in the same graph returns a wrong sum from its second replay on (the first
-    replay and eager runs are right; ``tools/probe_graph_reduce.py``: errors of 10^2 on sums of
+    replay and eager runs are right; the round-3 probe (profiles/r03/r03i/probe_graph_reduce.txt): errors of 10^2 on sums of
     ~10^3 at 8 192 and 65 536 rows, the GEMM output itself correct, the same sum as
     ``ones @ g`` correct). A Linear's bias gradient is exactly that column sum of the output
     gradient, so GraphedPPOUpdate's replays trained with wrong hidden-layer bias gradients."""
@@ -673,7 +673,7 @@ class GraphedPPOUpdate:
     ``fused`` (default: wherever ``PPOGrad`` supports the policy) takes the loss + backward from
     ``PPOGrad`` (rr_ppo_grad: one fp32-MFMA HIP pipeline) instead of PyTorch autograd, whose
     tall-skinny GEMMs over the 65 536-row minibatch run far below the GPU's rate (the weight
-    gradient dW = g^T x alone ~190 us per layer: tools/probe_bias_grad.py); the gradients then
+    gradient dW = g^T x alone ~190 us per layer: profiles/r03/r03i); the gradients then
     match the eager update's to fp32 rounding instead of bitwise. ``fused=False`` captures the
     PyTorch ops themselves (bitwise the eager ``ppo_update``).
 
@@ -715,7 +715,7 @@ class GraphedPPOUpdate:
         # static gradient buffers (allocated outside the graph): the captured step copies
         # torch.autograd.grad's results into them, so no accumulation into .grad is captured. The
         # policy's Linear layers must take their bias gradient as a GEMM (_LinearFn): a column sum
-        # after a GEMM in the same graph is wrong from the second replay on (tools/probe_graph_reduce.py)
+        # after a GEMM in the same graph is wrong from the second replay on (profiles/r03/r03i/probe_graph_reduce.txt)
         self.params = params
         for p in params:
             p.grad = torch.zeros_like(p)

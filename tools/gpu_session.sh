@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session of the round (phases in one gpurun call). Every GPU step has its own timeout;
 # a crash / timeout / abort ends the script (exit codes other than 0 / 1 stop it).
-#   tools/gpu_session.sh TAG "PHASES"   PHASES: any of tests bench dist prof pmc rollout exact
+#   tools/gpu_session.sh TAG "PHASES"   PHASES: any of tests bench dist prof pmc rollout floor exact
 #   (default: tests bench prof pmc rollout)
 TAG=${1:-run}
 PHASES=${2:-"tests bench prof pmc rollout"}
@@ -65,8 +65,15 @@ if has rollout; then
   (cd /tmp && step rp_rollout 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rp_rollout" -o bench -- python "$R/bench.py" --mode rollout --steps 320 > "$OUT/rp_rollout/bench.json" 2> "$OUT/rp_rollout/bench.err") || exit $?
   python tools/rocprof_step.py "$OUT/rp_rollout" --out "$OUT/rocprof_rollout_n65536_t16_fp32.json" > /dev/null
   cd /tmp || exit 2
-  step rollout_SQ 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/rollout_SQ" -o pmc -- python "$R/bench.py" --mode rollout --steps 64 > "$OUT/rollout_SQ.log" 2>&1
+  step rollout_SQ 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/rollout_SQ" -o pmc -- python "$R/bench.py" --mode rollout --steps 64 --no-ppo > "$OUT/rollout_SQ.log" 2>&1
   cd "$R" || exit 2
+fi
+if has floor; then
+  # the per-wave latency floor of the N = 65536 step kernel: probe kernels of its shape and memory
+  # pattern + the step itself, by events (back to back) and under the kernel tracer
+  step floor_ev 300 python tools/floor_probe.py run --out "$OUT/floor_events.json" > "$OUT/floor_events.log" 2>&1
+  mkdir -p "$OUT/floor_rp"
+  (cd /tmp && step floor_rp 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/floor_rp" -o fp -- python "$R/tools/floor_probe.py" run --reps 25 > "$OUT/floor_rp/run.log" 2>&1) || exit $?
 fi
 if has exact; then
   step bench_exact 300 $B --integrator dopri5 --steps 200 --warmup 10 --no-cpu-baseline --n-sweep "" > "$OUT/bench_exact.json" 2> "$OUT/bench_exact.err"

@@ -18,9 +18,9 @@ gcc -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-re
     -D_GNU_SOURCE -shared -o "$OUT/librocket_oracle_san.so" "$R/oracle/rocket_oracle.c" -lm || exit 2
 GASAN=$(gcc -print-file-name=libasan.so)
 GUBSAN=$(gcc -print-file-name=libubsan.so)
-echo "== oracle (gcc ASan+UBSan): tests/test_oracle_golden.py tests/test_params.py" | tee -a "$LOG"
+echo "== oracle (gcc ASan+UBSan): tests/test_oracle_golden.py tests/test_params.py tests/test_nonfinite.py (CPU part)" | tee -a "$LOG"
 (cd "$R" && RO_LIB_PATH="$OUT/librocket_oracle_san.so" LD_PRELOAD="$GASAN:$GUBSAN" \
-    python -m pytest -q -p no:cacheprovider tests/test_oracle_golden.py tests/test_params.py 2>&1) | tee -a "$LOG" | tail -3
+    python -m pytest -v -p no:cacheprovider -m "not gpu" tests/test_oracle_golden.py tests/test_params.py tests/test_nonfinite.py 2>&1) | tee -a "$LOG" | tail -4
 rc1=$?
 # 2. librocket_hip host code: hipcc -Xarch_host -fsanitize=address,undefined
 (cd "$R" && python -c "
@@ -33,7 +33,7 @@ subprocess.check_call(cmd)
 CASAN=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
 echo "== librocket_hip host code (clang ASan+UBSan): tests/test_capi.py" | tee -a "$LOG"
 (cd "$R" && RR_LIB_PATH="$OUT/librocket_hip_san.so" LD_PRELOAD="$CASAN" \
-    python -m pytest -q -p no:cacheprovider tests/test_capi.py -k "not library_exports" 2>&1) | tee -a "$LOG" | tail -3
+    python -m pytest -v -p no:cacheprovider tests/test_capi.py -k "not library_exports" 2>&1) | tee -a "$LOG" | tail -4
 rc2=$?
 echo "oracle rc=$rc1 host-abi rc=$rc2" | tee -a "$LOG"
 [ $rc1 -eq 0 ] && [ $rc2 -eq 0 ]
