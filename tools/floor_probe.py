@@ -1,6 +1,6 @@
 """The per-wave latency floor of the N = 65 536 step kernel.
 
-    python tools/floor_probe.py run [--n 65536] [--out FILE]          # events, back to back
+    python tools/floor_probe.py run --graph [--n 65536] [--out FILE]  # events, back to back (hipGraph)
     rocprofv3 --kernel-trace --stats --output-format csv -d DIR -o fp -- python tools/floor_probe.py run --reps 25
     python tools/floor_probe.py model RUN.json DIR/fp_kernel_stats.csv [--out FILE]
 
@@ -8,7 +8,8 @@
 launch shape and memory pattern: empty, memory only, memory + 128 / 256 / 384 / 512 VALU of
 dependent fma chains) and the real step kernel (rr_step through RocketBatch at N envs, auto-reset,
 TimeLimit 800 — the bench's headline configuration), each `reps` times back to back after a
-warm-up, and prints the per-launch time by HIP events around each back-to-back group. Under
+warm-up, and prints the per-launch time by HIP events around each back-to-back group (--graph:
+replayed from a hipGraph, so the host does not pace them). Under
 rocprofv3 the same command gives every kernel's kernel-trace duration. `model` fits
 t(VALU) = t_mem + c * VALU over the probe chain (c = cycles per lone-wave VALU instruction at the
 clock the chip held) and places the step kernel on it with the VALU count of its slowest wave
@@ -48,16 +49,33 @@ def run(a):
     reward = torch.empty((n,), device=dev)
     done = torch.empty((n,), device=dev, dtype=torch.uint8)
     trunc = torch.empty((n,), device=dev, dtype=torch.uint8)
-    stream = torch.cuda.current_stream(dev)
     ptr = lambda t: P(t.data_ptr())  # noqa: E731
-    out = {"n": n, "reps": a.reps, "events_us_per_launch": {}}
+    out = {"n": n, "reps": a.reps, "launch": "hipGraph of reps launches" if a.graph else "direct launches",
+           "events_us_per_launch": {}}
 
     def timed(fn):
+        """Per-launch time of `reps` back-to-back launches by HIP events: replayed from one hipGraph
+        (--graph: the host cannot pace them; the replay's fixed preamble is spread over the reps), or
+        issued directly (host-paced for launches shorter than the ~3 us of host time each costs)."""
+        stream = torch.cuda.current_stream(dev)
         fn(5)  # warm-up
         torch.cuda.synchronize(dev)
+        if a.graph:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(stream)
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    fn(a.reps)
+            stream.wait_stream(s)
+            g.replay()
+            torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        fn(a.reps)
+        if a.graph:
+            g.replay()
+        else:
+            fn(a.reps)
         e1.record(stream)
         torch.cuda.synchronize(dev)
         return e0.elapsed_time(e1) / a.reps * 1e3
@@ -65,7 +83,7 @@ def run(a):
     for kind, name in KINDS.items():
         def probe(k, kind=kind):
             rc = lib.fp_repeat(kind, k, ptr(state), ptr(action), n, ptr(obs), ptr(reward), ptr(done), ptr(trunc),
-                               P(stream.cuda_stream))
+                               P(torch.cuda.current_stream(dev).cuda_stream))
             if rc:
                 raise RuntimeError("fp_repeat(%d): %d" % (kind, rc))
         out["events_us_per_launch"][name] = timed(probe)
@@ -170,6 +188,7 @@ def main():
     r = sub.add_parser("run")
     r.add_argument("--n", type=int, default=65536)
     r.add_argument("--reps", type=int, default=200)
+    r.add_argument("--graph", action="store_true", help="time hipGraph replays (the unprofiled back-to-back frame)")
     r.add_argument("--out")
     m = sub.add_parser("model")
     m.add_argument("run")

@@ -71,7 +71,7 @@ fi
 if has floor; then
   # the per-wave latency floor of the N = 65536 step kernel: probe kernels of its shape and memory
   # pattern + the step itself, by events (back to back) and under the kernel tracer
-  step floor_ev 300 python tools/floor_probe.py run --out "$OUT/floor_events.json" > "$OUT/floor_events.log" 2>&1
+  step floor_ev 300 python tools/floor_probe.py run --graph --out "$OUT/floor_events.json" > "$OUT/floor_events.log" 2>&1
   mkdir -p "$OUT/floor_rp"
   (cd /tmp && step floor_rp 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/floor_rp" -o fp -- python "$R/tools/floor_probe.py" run --reps 25 > "$OUT/floor_rp/run.log" 2>&1) || exit $?
 fi
