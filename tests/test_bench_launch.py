@@ -97,3 +97,32 @@ def test_episode_analyzer_statistics_host():
 
     assert isinstance(u.get_trajectory_plotly(), go.Figure)
     assert isinstance(u.get_vtarg_trajectory(), go.Figure)
+
+
+def test_host_cores_uses_the_affinity_mask_narrowed_by_quota_and_omp(monkeypatch):
+    """cpu_baseline's all-cores leg: the affinity count, narrowed by the cgroup CPU quota and
+    OMP_NUM_THREADS when set (no fixed cap), with where the count came from."""
+    import bench
+
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(40)))
+    monkeypatch.setattr(bench, "_cgroup_cpus", lambda: None)
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    assert bench.host_cores() == (40, {"affinity": 40})
+    monkeypatch.setattr(bench, "_cgroup_cpus", lambda: 24)
+    assert bench.host_cores() == (24, {"affinity": 40, "cgroup_quota": 24})
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert bench.host_cores() == (16, {"affinity": 40, "cgroup_quota": 24, "OMP_NUM_THREADS": 16})
+
+
+def test_rollout_roofline_counts():
+    """The configs[4] roofline's algorithmic counts: SB3 MlpPolicy (64x64) towers' GEMM FLOPs per
+    env-step and the collect's HBM bytes per env-step."""
+    import bench
+
+    # pi: 14*64 + 64*64 + 64*3 MACs, vf: 14*64 + 64*64 + 64*1 MACs, 2 FLOP each
+    assert bench.rollout_flops_per_env_step(14, 3) == 2 * (896 + 4096 + 192) + 2 * (896 + 4096 + 64) == 20480
+    assert bench.rollout_flops_per_env_step(7, 2) == 2 * (448 + 4096 + 128) + 2 * (448 + 4096 + 64)
+    # buffer slices per step: obs 56 + action 12 + value / log-prob / start / reward / adv / ret 24
+    b16 = bench.rollout_bytes_per_env_step(14, 3, 16)
+    assert bench.rollout_bytes_per_env_step(14, 3, 10 ** 9) == pytest.approx(92.0)
+    assert 92.0 < b16 < 110.0
