@@ -49,6 +49,15 @@ class HostArray:
             pass
 
 
+class OutputSet(tuple):
+    """(obs, reward, done, truncated) device views of one contiguous block (`block`, uint8)."""
+
+    def __new__(cls, views, block):
+        self = super().__new__(cls, views)
+        self.block = block
+        return self
+
+
 class RocketBatch:
     def __init__(self, num_envs, model="6DOF", device=None, max_episode_steps=0, auto_reset=True,
                  episode_stats=True, reward_annealing=False, integrator="rk4", env_id_offset=0,
@@ -85,13 +94,10 @@ class RocketBatch:
                                       device.index), "rr_create")
         self._h = h
         self.env_id_offset = int(env_id_offset)
-        n, ns = self.num_envs, self.state_dim
-        kw = dict(device=device)
-        self.obs = torch.empty((n, ns), dtype=torch.float32, **kw)
-        self.reward = torch.empty((n,), dtype=torch.float32, **kw)
-        self.done = torch.empty((n,), dtype=torch.uint8, **kw)
-        self.truncated = torch.empty((n,), dtype=torch.uint8, **kw)
-        self.terms = torch.empty((self.n_terms + 2, n), dtype=torch.float32, **kw) if compute_terms else None
+        n = self.num_envs
+        self.outputs = self.alloc_outputs()
+        self.obs, self.reward, self.done, self.truncated = self.outputs
+        self.terms = torch.empty((self.n_terms + 2, n), dtype=torch.float32, device=device) if compute_terms else None
         self.seed(self.cfg.kwargs["seed"] if seed is None else seed)
 
     # -- plumbing ---------------------------------------------------------------------------------------------
@@ -151,11 +157,15 @@ class RocketBatch:
         return obs
 
     def alloc_outputs(self):
-        """A fresh set of step output tensors (obs, reward, done, truncated) for step(out=...)."""
+        """A fresh set of step output tensors (obs [N,ns] f32, reward [N] f32, done [N] u8, truncated
+        [N] u8) for step(out=...): views of ONE contiguous device block in that order, so that a
+        host copy of all four is one DMA (the returned tuple's `.block`)."""
         t = self.torch
         n, ns = self.num_envs, self.state_dim
-        return (t.empty((n, ns), dtype=t.float32, device=self.device), t.empty((n,), dtype=t.float32, device=self.device),
-                t.empty((n,), dtype=t.uint8, device=self.device), t.empty((n,), dtype=t.uint8, device=self.device))
+        o_b, r_b = 4 * n * ns, 4 * n
+        blk = t.empty((o_b + r_b + 2 * n,), dtype=t.uint8, device=self.device)
+        return OutputSet((blk[:o_b].view(t.float32).view(n, ns), blk[o_b:o_b + r_b].view(t.float32),
+                          blk[o_b + r_b:o_b + r_b + n], blk[o_b + r_b + n:]), blk)
 
     def step(self, action, out=None):
         """One env step for all envs. Returns the output tensors (obs [N,ns], reward [N], done

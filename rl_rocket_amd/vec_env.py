@@ -302,14 +302,20 @@ class RocketVecEnv(_VecEnvBase):
 
     def _to_host(self, obs, rew, done, trunc):
         """The four step outputs as numpy views of one fresh pinned block (obs [N][ns] f32,
-        reward [N] f32, done [N] bool, truncated [N] u8), after one stream synchronise."""
+        reward [N] f32, done [N] bool, truncated [N] u8), after one stream synchronise. The
+        batch's outputs are views of one device block in the same layout (RocketBatch.alloc_outputs),
+        so this is ONE DMA copy."""
         t, n, ns = self.batch.torch, self.num_envs, self.batch.state_dim
         o_b, r_b = 4 * n * ns, 4 * n
         blk = t.empty((o_b + r_b + 2 * n,), dtype=t.uint8, pin_memory=True)
         views = (blk[:o_b].view(t.float32).view(n, ns), blk[o_b:o_b + r_b].view(t.float32),
                  blk[o_b + r_b:o_b + r_b + n], blk[o_b + r_b + n:])
-        for dst, src in zip(views, (obs, rew, done, trunc)):
-            dst.copy_(src, non_blocking=True)
+        src_blk = getattr(getattr(self.batch, "outputs", None), "block", None)
+        if src_blk is not None and obs is self.batch.obs:
+            blk.copy_(src_blk, non_blocking=True)
+        else:
+            for dst, src in zip(views, (obs, rew, done, trunc)):
+                dst.copy_(src, non_blocking=True)
         t.cuda.current_stream(self.batch.device).synchronize()
         o, r, d, tr = (v.numpy() for v in views)
         return o, r, d.view(np.bool_), tr  # the kernel writes done as 0 / 1

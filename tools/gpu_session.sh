@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session of the round (phases in one gpurun call). Every GPU step has its own timeout;
 # a crash / timeout / abort ends the script (exit codes other than 0 / 1 stop it).
-#   tools/gpu_session.sh TAG "PHASES"   PHASES: any of tests bench dist prof pmc rollout floor exact
+#   tools/gpu_session.sh TAG "PHASES"   PHASES: any of tests bench dist prof pmc rollout legs floor exact
 #   (default: tests bench prof pmc rollout)
 TAG=${1:-run}
 PHASES=${2:-"tests bench prof pmc rollout"}
@@ -67,6 +67,15 @@ if has rollout; then
   cd /tmp || exit 2
   step rollout_SQ 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/rollout_SQ" -o pmc -- python "$R/bench.py" --mode rollout --steps 64 --no-ppo > "$OUT/rollout_SQ.log" 2>&1
   cd "$R" || exit 2
+fi
+if has legs; then
+  # the other configurations: configs[1] (3DOF Euler, N = 4096), 3DOF RK4 at 524288, the rollout's
+  # faster tower precisions
+  step legs_cfg1 300 $B --model 3DOF --integrator euler --n 4096 --steps 20 --warmup 5 --no-cpu-baseline --n-sweep "" > "$OUT/legs_cfg1_3dof_euler_n4096.json" 2> "$OUT/legs_cfg1.err"
+  step legs_3dof_rk4 300 $B --model 3DOF --n 524288 --steps 20 --warmup 5 --no-cpu-baseline --n-sweep "" > "$OUT/legs_3dof_rk4_n524288.json" 2> "$OUT/legs_3dof.err"
+  for P in fp16x3 bf16; do
+    step legs_rollout_$P 300 $B --mode rollout --steps 320 --policy-dtype $P --no-ppo > "$OUT/legs_rollout_$P.json" 2> "$OUT/legs_rollout_$P.err"
+  done
 fi
 if has floor; then
   # the per-wave latency floor of the N = 65536 step kernel: probe kernels of its shape and memory
