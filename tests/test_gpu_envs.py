@@ -117,10 +117,19 @@ def test_vec_env_sb3_semantics():
                 assert not t_trunc[i]
         for i in np.nonzero(~done)[0][:50]:
             assert infos[i] == {}
+        if k % 30 == 0:  # SB3's iteration (_update_info_buffer): the same dicts, every env its own
+            lst = list(infos)
+            assert len(lst) == n and all(lst[i] is infos[i] for i in idx)
+            assert sum(1 for d in lst if d.get("episode") is not None) == len(idx)
         ep_ret[idx] = 0
         ep_len[idx] = 0
     assert seen_trunc and seen_term
     assert env.episode_lengths and len(env.episode_lengths) == len(env.episode_returns)
+    # the host outputs come from ONE DMA of the batch's contiguous output block
+    b = env.batch
+    blk = b.outputs.block
+    assert b.obs.data_ptr() == blk.data_ptr() and b.reward.data_ptr() == blk.data_ptr() + 4 * n * 14
+    assert b.truncated.data_ptr() + n == blk.data_ptr() + blk.numel()
     env.close()
     twin.close()
 
