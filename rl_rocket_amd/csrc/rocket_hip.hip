@@ -2220,23 +2220,12 @@ int launch_rollout(rr_env* e, const char* who, bool multi, const float* params, 
     const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
     const dim3 grid((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock));
     // 64 envs per wave (two 32-env MFMA column tiles). 32 envs per wave (rol::Shape<1>, two waves
-    // per SIMD) measured 2-16 % slower at N = 65536 in round 2: the env step's VALU work doubles.
+    // per SIMD) measured 2-16 % slower at N = 65536 in round 2 and 4-8 % slower in round 4, with or
+    // without the second wave's start staggered: the env step's VALU work doubles, and an fp32
+    // MFMA holds its SIMD's vector issue, so one wave's MFMAs do not hide the other's VALU work
+    // (tools/coissue_probe.hip, profiles/r04/coissue/).
     hipStream_t s = (hipStream_t)stream;
     const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
-    {  // A/B (round 4): 32 envs per wave, two waves per SIMD, the second one's start staggered
-        const char* nt = std::getenv("RR_ROLLOUT_NTW");
-        const char* st = std::getenv("RR_ROLLOUT_STAGGER");
-        io.stagger = st ? (uint32_t)std::strtoul(st, nullptr, 10) : 0u;
-        if (nt && nt[0] == '1' && multi && m6 && !euler && precision == RR_POLICY_FP32) {
-            const dim3 g1((unsigned)((e->n + rol::kEnvsPerBlock - 1) / rol::kEnvsPerBlock));
-            hipLaunchKernelGGL((rollout_step_kernel<6, RR_INT_RK4, 0, true, 1>), g1, dim3(rol::Shape<1>::kThreads), 0,
-                               s, e->state, nn, mode, e->kp, b, io);
-            hipError_t err = hipGetLastError();
-            if (err != hipSuccess) return hip_fail(err, (std::string(who) + ": launch").c_str());
-            e->steps += io.T;
-            return RR_OK;
-        }
-    }
 #define RR_LAUNCH(M, I, PR)                                                                                        \
     do {                                                                                                           \
         if (!multi)                                                                                                \
