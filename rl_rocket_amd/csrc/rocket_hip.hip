@@ -1063,7 +1063,9 @@ __device__ __forceinline__ void store_outputs(const StepIO& io, uint32_t i, uint
 // ROWS (rr_step_rows): obs, reward and done leave as ONE row of NS + 2 fp32 per env
 // (obs[NS], reward, done as 0 / 1) through the same LDS tile, e.g. straight into the send
 // buffer of the multi-GPU all-gather (rl_rocket_amd.dist.ShardGather).
-#ifndef RR_TU_EXACT  // rocket_exact.hip compiles this file again for the exact-mode kernels only
+// rocket_exact.hip compiles this file again for the exact-mode kernels only, rocket_collect.hip for
+// the rollout collect kernels only
+#if !defined(RR_TU_EXACT) && !defined(RR_TU_COLLECT)
 template <int MODEL, int INTEG, bool ASOA, bool HELP, int WPB, bool ROWS>
 // amdgpu_waves_per_eu(4): <= 128 VGPRs keeps 4 waves per SIMD at large N
 __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(
@@ -1284,11 +1286,16 @@ __global__ __launch_bounds__(kBlock) void copy_done_rows_kernel(const uint64_t* 
     if (d_len) d_len[i] = term_len[i];
 }
 
+#endif  // !RR_TU_EXACT && !RR_TU_COLLECT
+
+#ifndef RR_TU_EXACT
 // On-device PPO rollout kernels (fused MlpPolicy forward on fp32 MFMA, bootstrap, GAE)
 #include "rocket_policy.inc"
 #include "rocket_rollout.inc"
+#ifndef RR_TU_COLLECT
 // PPO minibatch gradient (loss + backward of the MlpPolicy on fp32 MFMA)
 #include "rocket_ppo.inc"
+#endif  // RR_TU_COLLECT
 #endif  // RR_TU_EXACT
 
 // Exact-integrator mode (RR_INT_DOPRI5): fp64 scipy RK45 restatement, compiled without
@@ -1319,12 +1326,56 @@ extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model,
         hipLaunchKernelGGL(step_exact_kernel<3>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, x, b, o, state64);
     return (int)hipGetLastError();
 }
+#elif defined(RR_TU_COLLECT)
+}  // namespace
+
+// the collect TU's only entry point (hidden: not part of the C-ABI): one rr_rollout_collect launch,
+// rollout_step_kernel<MODEL, INTEG, PREC, MULTI = true, 2>. kp / bufs / io point to the KParams /
+// Bufs / RolloutIO of the calling TU (same definitions, same layout).
+extern "C" __attribute__((visibility("hidden"))) int rrc_launch_collect(int model, int integ, int prec,
+                                                                          unsigned grid, float* state, uint32_t n,
+                                                                          uint32_t mode, const void* kp,
+                                                                          const void* bufs, const void* io,
+                                                                          void* stream)
+{
+    KParams p;
+    Bufs b;
+    RolloutIO o;
+    std::memcpy(&p, kp, sizeof(KParams));
+    std::memcpy(&b, bufs, sizeof(Bufs));
+    std::memcpy(&o, io, sizeof(RolloutIO));
+    hipStream_t s = (hipStream_t)stream;
+#define RR_COLLECT(M, I, PR)                                                                                  \
+    hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true, 2>), dim3(grid), dim3(rol::Shape<2>::kThreads), 0, \
+                       s, state, n, mode, p, b, o)
+#define RR_COLLECT_P(M, I)                      \
+    do {                                        \
+        if (prec == 1) RR_COLLECT(M, I, 1);     \
+        else if (prec == 2) RR_COLLECT(M, I, 2); \
+        else RR_COLLECT(M, I, 0);               \
+    } while (0)
+    const bool euler = integ == RR_INT_EULER;
+    if (model == RR_MODEL_6DOF && !euler) RR_COLLECT_P(6, RR_INT_RK4);
+    else if (model == RR_MODEL_6DOF) RR_COLLECT_P(6, RR_INT_EULER);
+    else if (!euler) RR_COLLECT_P(3, RR_INT_RK4);
+    else RR_COLLECT_P(3, RR_INT_EULER);
+#undef RR_COLLECT_P
+#undef RR_COLLECT
+    return (int)hipGetLastError();
+}
 #else  // the main translation unit: host side
 
-// defined by the exact translation unit; this weak stand-in (a library built from this file alone,
-// e.g. a tools/ A/B variant) makes RR_INT_DOPRI5 steps fail loudly instead of failing to load
+// defined by the exact / collect translation units; these weak stand-ins (a library built from this
+// file alone, e.g. a tools/ A/B variant) make RR_INT_DOPRI5 steps and rr_rollout_collect fail loudly
+// instead of failing to load
 extern "C" __attribute__((weak, visibility("hidden"))) int rrx_launch_exact(int, const void*, const void*,
                                                                           const void*, double*, unsigned, void*)
+{
+    return (int)hipErrorInvalidDeviceFunction;
+}
+extern "C" __attribute__((weak, visibility("hidden"))) int rrc_launch_collect(int, int, int, unsigned, float*,
+                                                                            uint32_t, uint32_t, const void*,
+                                                                            const void*, const void*, void*)
 {
     return (int)hipErrorInvalidDeviceFunction;
 }
@@ -2224,30 +2275,33 @@ int launch_rollout(rr_env* e, const char* who, bool multi, const float* params, 
     // without the second wave's start staggered: the env step's VALU work doubles, and an fp32
     // MFMA holds its SIMD's vector issue, so one wave's MFMAs do not hide the other's VALU work
     // (tools/coissue_probe.hip, profiles/r04/coissue/).
+    // The collect kernel (MULTI) lives in the third translation unit (rocket_collect.hip), compiled
+    // with the MFMA accumulators in VGPRs (rl_rocket_amd/build.py COLLECT_FLAGS).
     hipStream_t s = (hipStream_t)stream;
-    const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
-#define RR_LAUNCH(M, I, PR)                                                                                        \
-    do {                                                                                                           \
-        if (!multi)                                                                                                \
-            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, false, 2>), grid, dim3(rol::Shape<2>::kThreads), 0, \
-                               s, e->state, nn, mode, e->kp, b, io);                                               \
-        else                                                                                                       \
-            hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, true, 2>), grid, dim3(rol::Shape<2>::kThreads), 0,  \
-                               s, e->state, nn, mode, e->kp, b, io);                                               \
+    const int prec = precision == RR_POLICY_BF16 ? 1 : precision == RR_POLICY_FP16X3 ? 2 : 0;
+    hipError_t err = hipSuccess;
+    if (multi) {
+        err = (hipError_t)rrc_launch_collect(e->p.model, e->p.integrator, prec, grid.x, e->state, nn, mode, &e->kp,
+                                             &b, &io, stream);
+    } else {
+        const bool m6 = e->p.model == RR_MODEL_6DOF, euler = e->p.integrator == RR_INT_EULER;
+#define RR_LAUNCH(M, I, PR)                                                                                     \
+    hipLaunchKernelGGL((rollout_step_kernel<M, I, PR, false, 2>), grid, dim3(rol::Shape<2>::kThreads), 0, s, \
+                       e->state, nn, mode, e->kp, b, io)
+#define RR_LAUNCH_P(M, I)                  \
+    do {                                   \
+        if (prec == 1) RR_LAUNCH(M, I, 1); \
+        else if (prec == 2) RR_LAUNCH(M, I, 2); \
+        else RR_LAUNCH(M, I, 0);           \
     } while (0)
-#define RR_LAUNCH_P(M, I)                                           \
-    do {                                                            \
-        if (precision == RR_POLICY_BF16) RR_LAUNCH(M, I, 1);        \
-        else if (precision == RR_POLICY_FP16X3) RR_LAUNCH(M, I, 2); \
-        else RR_LAUNCH(M, I, 0);                                    \
-    } while (0)
-    if (m6 && !euler) RR_LAUNCH_P(6, RR_INT_RK4);
-    else if (m6) RR_LAUNCH_P(6, RR_INT_EULER);
-    else if (!euler) RR_LAUNCH_P(3, RR_INT_RK4);
-    else RR_LAUNCH_P(3, RR_INT_EULER);
+        if (m6 && !euler) RR_LAUNCH_P(6, RR_INT_RK4);
+        else if (m6) RR_LAUNCH_P(6, RR_INT_EULER);
+        else if (!euler) RR_LAUNCH_P(3, RR_INT_RK4);
+        else RR_LAUNCH_P(3, RR_INT_EULER);
 #undef RR_LAUNCH_P
 #undef RR_LAUNCH
-    hipError_t err = hipGetLastError();
+        err = hipGetLastError();
+    }
     if (err != hipSuccess) return hip_fail(err, (std::string(who) + ": launch").c_str());
     e->steps += io.T;
     return RR_OK;
