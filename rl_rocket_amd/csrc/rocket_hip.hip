@@ -57,6 +57,9 @@ constexpr int kOutAux = 16;
 constexpr int64_t kHelpMaxN = 131072;
 // largest N stepped with one main wave per workgroup (helper variant)
 constexpr int64_t kNarrowMaxN = 16384;
+// largest N of the exact mode's one-wave-per-SIMD 6DOF kernel (256 CUs x 4 SIMDs x 64 lanes:
+// one env per lane); above it the lean two-waves-per-SIMD kernel (rocket_dopri5.inc, solve LEAN)
+constexpr int64_t kExactLeanMinN = 256 * 4 * 64;
 constexpr int kWave = 64;
 constexpr int kBlock = 256;  // threads per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
@@ -1311,19 +1314,25 @@ __global__ __launch_bounds__(kBlock) void copy_done_rows_kernel(const uint64_t* 
 
 // the exact TU's only entry point (hidden: not part of the C-ABI). bufs / io / xp point to the
 // Bufs / StepIO / XParams of the calling TU (same definitions, same layout).
-extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model, const void* xp, const void* bufs,
-                                                                        const void* io, double* state64,
-                                                                        unsigned grid, void* stream)
+extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model, int lean, const void* xp,
+                                                                        const void* bufs, const void* io,
+                                                                        double* state64, unsigned grid, void* stream)
 {
     Bufs b;
     StepIO o;
     std::memcpy(&b, bufs, sizeof(Bufs));
     std::memcpy(&o, io, sizeof(StepIO));
     const XParams* x = static_cast<const XParams*>(xp);
-    if (model == RR_MODEL_6DOF)
-        hipLaunchKernelGGL(step_exact_kernel<6>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, x, b, o, state64);
+    hipStream_t s = (hipStream_t)stream;
+    // lean (6DOF above one wave per SIMD, the caller's choice): 256 registers, two waves per SIMD
+    // hide each other's fp64 latency (147.6 vs 176.6 us at N = 524 288); otherwise the in-loop
+    // dense output (no event re-derivation, no spills: 28.9 vs 32.1 us at 65 536), profiles/r04/ab_lean/
+    if (model == RR_MODEL_6DOF && lean)
+        hipLaunchKernelGGL((step_exact_kernel<6, true>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);
+    else if (model == RR_MODEL_6DOF)
+        hipLaunchKernelGGL((step_exact_kernel<6, false>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);
     else
-        hipLaunchKernelGGL(step_exact_kernel<3>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, x, b, o, state64);
+        hipLaunchKernelGGL((step_exact_kernel<3, false>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);
     return (int)hipGetLastError();
 }
 #elif defined(RR_TU_COLLECT)
@@ -1368,7 +1377,7 @@ extern "C" __attribute__((visibility("hidden"))) int rrc_launch_collect(int mode
 // defined by the exact / collect translation units; these weak stand-ins (a library built from this
 // file alone, e.g. a tools/ A/B variant) make RR_INT_DOPRI5 steps and rr_rollout_collect fail loudly
 // instead of failing to load
-extern "C" __attribute__((weak, visibility("hidden"))) int rrx_launch_exact(int, const void*, const void*,
+extern "C" __attribute__((weak, visibility("hidden"))) int rrx_launch_exact(int, int, const void*, const void*,
                                                                           const void*, double*, unsigned, void*)
 {
     return (int)hipErrorInvalidDeviceFunction;
@@ -1539,6 +1548,7 @@ struct rr_env {
     int64_t n, id_off;
     uint64_t steps;
     int64_t help_max_n;       // largest N stepped with helper waves (kHelpMaxN, RR_HELP_MAX_N env override)
+    int64_t exact_lean_min_n; // 6DOF exact mode: lean kernel above this N (kExactLeanMinN, RR_EXACT_LEAN_MIN_N)
     float* state;
     float* v0;
     uint32_t* counter;
@@ -1629,6 +1639,9 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
         // test / A-B override of the helper-wave threshold: RR_HELP_MAX_N=<n> in the environment
         const char* hv = std::getenv("RR_HELP_MAX_N");
         e->help_max_n = hv ? std::strtoll(hv, nullptr, 10) : kHelpMaxN;
+        // the same for the exact mode's lean-kernel threshold (tests run the lean kernel at small N)
+        const char* lv = std::getenv("RR_EXACT_LEAN_MIN_N");
+        e->exact_lean_min_n = lv ? std::strtoll(lv, nullptr, 10) : kExactLeanMinN;
     }
     DeviceGuard g(device);
     struct A {
@@ -1787,7 +1800,8 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     if (e->p.integrator == RR_INT_DOPRI5) {
         // the exact kernels live in the second translation unit (rocket_exact.hip: compiled with a
         // register-pressure-first scheduler, no scratch spills)
-        const hipError_t xe = (hipError_t)rrx_launch_exact(m6 ? RR_MODEL_6DOF : RR_MODEL_3DOF, e->d_xp, &b, &io,
+        const hipError_t xe = (hipError_t)rrx_launch_exact(m6 ? RR_MODEL_6DOF : RR_MODEL_3DOF,
+                                                           m6 && e->n > e->exact_lean_min_n, e->d_xp, &b, &io,
                                                            e->state64, grid.x, s);
         if (xe != hipSuccess) return hip_fail(xe, "rr_step: exact launch");
     } else {

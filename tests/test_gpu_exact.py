@@ -14,6 +14,15 @@ REWARD_TOL = 1e-7    # floored-relative |a-b|/max(|b|,1): reward / terms are ret
 OBS_TOL = 1e-7
 
 
+@pytest.fixture(params=[False, True], ids=["inloop", "lean"])
+def lean(request, monkeypatch):
+    """Both 6DOF exact kernels: the in-loop dense output (N <= 65 536) and the lean
+    two-waves-per-SIMD kernel (above it; RR_EXACT_LEAN_MIN_N=0 selects it at any N)."""
+    if request.param:
+        monkeypatch.setenv("RR_EXACT_LEAN_MIN_N", "0")
+    return request.param
+
+
 def _kw(model):
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
     return ENV_CONFIG_6DOF if model == 6 else {}
@@ -65,14 +74,14 @@ def _check(model, ref, out, norm, label, reward_tol=REWARD_TOL):
 
 
 @pytest.mark.parametrize("model", [6, 3])
-def test_exact_vs_reference_primary(model, golden6, golden3):
+def test_exact_vs_reference_primary(model, golden6, golden3, lean):
     g = golden6 if model == 6 else golden3
     out = run_exact(model, g, clamp=False, **_kw(model))
     _check(model, g, out, g["normalizer"], "DOPRI5 %dDOF vs reference (numpy 1.26 / scipy 1.7)" % model)
 
 
 @pytest.mark.parametrize("model", [6, 3])
-def test_exact_vs_reference_cross_stack(model, golden6, golden3, golden6_x, golden3_x):
+def test_exact_vs_reference_cross_stack(model, golden6, golden3, golden6_x, golden3_x, lean):
     g = golden6 if model == 6 else golden3
     x = dict(golden6_x if model == 6 else golden3_x)
     out = run_exact(model, g, clamp=True, **_kw(model))
@@ -93,8 +102,25 @@ def test_exact_vs_oracle_65536(oracle_mod):
     _check(6, ref, out, np.array(cfg.normalizer[:14]), "DOPRI5 6DOF vs oracle N=65536")
 
 
+def test_exact_lean_kernel_is_bitwise_the_inloop_kernel(monkeypatch):
+    """The lean kernel re-derives an event step's stages after the step loop: same inputs, same
+    arithmetic, so every output is bitwise the in-loop kernel's, event rows included."""
+    from test_gpu_parity import _random_states6
+
+    n = 65536
+    ic, s, a = _random_states6(n, seed=12)
+    rows = dict(ic=ic, state_in=s, action=a, t_in=np.zeros(n))
+    ref = run_exact(6, rows, **_kw(6))
+    monkeypatch.setenv("RR_EXACT_LEAN_MIN_N", "0")
+    out = run_exact(6, rows, **_kw(6))
+    print("event rows", int(ref["event"].sum()), "done rows", int(ref["done"].sum()))
+    assert ref["event"].sum() > 100
+    for k in ("state_out", "state32", "obs", "reward", "terms", "done", "bounds_violation", "event"):
+        assert np.array_equal(out[k], ref[k], equal_nan=out[k].dtype.kind == "f"), k
+
+
 @pytest.mark.parametrize("model", [6, 3])
-def test_exact_trajectories(model, golden6, golden3):
+def test_exact_trajectories(model, golden6, golden3, lean):
     """G7 50-step trajectories chained on the GPU in fp64 (clock from the counter word):
     the exact mode carries the reference's float64 state, so there is no fp32 drift."""
     import torch

@@ -19,11 +19,13 @@ def hashes():
     return B.kernel_isa_hashes(B.OUT)
 
 
-def test_both_translation_units_hashed(hashes):
+def test_every_translation_unit_hashed(hashes):
     names = list(hashes)
-    assert any("step_kernel<6, 0, false, true, 4, false>" in k for k in names)
-    assert any("step_exact_kernel<6>" in k for k in names)
-    assert any("rollout_step_kernel" in k for k in names)
+    assert any("step_kernel<6, 0, false, true, 4, false>" in k for k in names)  # main
+    assert any("step_exact_kernel<6, true>" in k for k in names)  # exact
+    assert any("step_exact_kernel<6, false>" in k for k in names)
+    assert any("rollout_step_kernel<6, 0, 0, false" in k for k in names)  # main
+    assert any("rollout_step_kernel<6, 0, 0, true" in k for k in names)  # collect
     assert all(len(v) == 16 for v in hashes.values())
 
 
