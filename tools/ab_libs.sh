@@ -4,13 +4,18 @@
 # then timed, interleaved over two repetitions.
 #   tools/ab_libs.sh TAG rollout NAME...   rollout collect (--no-ppo), us per collect
 #   tools/ab_libs.sh TAG exact NAME...     exact mode at N = 65 536 and 524 288, ms per step
+#   tools/ab_libs.sh TAG ppo NAME...       fused PPO minibatch update (rollout bench with PPO), ms
 TAG=${1:-ab}; MODE=${2:-rollout}; shift 2
 NAMES=${*:-"base"}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 2
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
-if [ "$MODE" = rollout ]; then TESTS=tests/test_gpu_rollout.py; else TESTS=tests/test_gpu_exact.py; fi
+case "$MODE" in
+  rollout) TESTS=tests/test_gpu_rollout.py ;;
+  ppo) TESTS=tests/test_gpu_ppo.py ;;
+  *) TESTS=tests/test_gpu_exact.py ;;
+esac
 chk() {  # chk NAME: parity tests against this library
   RR_LIB_PATH="$R/tools/ab/lib_$1.so" timeout -k 10 300 python -u -m pytest "$TESTS" -x -q \
     --timeout 120 --timeout-method thread -m gpu > "$OUT/test_$1.log" 2>&1
@@ -23,6 +28,9 @@ run() {  # run NAME REP [N]
   if [ "$MODE" = rollout ]; then
     RR_LIB_PATH="$R/tools/ab/lib_$1.so" timeout -k 10 200 python bench.py --mode rollout --steps 320 --no-ppo \
       > "$OUT/$tag.json" 2> "$OUT/$tag.err"
+  elif [ "$MODE" = ppo ]; then
+    RR_LIB_PATH="$R/tools/ab/lib_$1.so" timeout -k 10 300 python bench.py --mode rollout --steps 32 \
+      > "$OUT/$tag.json" 2> "$OUT/$tag.err"
   else
     RR_LIB_PATH="$R/tools/ab/lib_$1.so" timeout -k 10 200 python bench.py --integrator dopri5 --n "$3" --steps 50 \
       --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$OUT/$tag.json" 2> "$OUT/$tag.err"
@@ -30,11 +38,11 @@ run() {  # run NAME REP [N]
   local rc=$?
   echo "[$tag] exit $rc" | tee -a "$OUT/status.txt"
   if [ "$rc" -ne 0 ]; then echo "stopping after $tag (rc=$rc)"; exit "$rc"; fi
-  python -c "import json,sys; d=[json.loads(x) for x in open(sys.argv[1]) if x.startswith('{')][-1]; v=d.get('gpu_ms_per_collect'); print(sys.argv[2], round((v if v is not None else d['ms_per_step'])*1e3, 2), 'us per', 'collect' if v is not None else 'step')" "$OUT/$tag.json" "$tag" | tee -a "$OUT/summary.txt"
+  python -c "import json,sys; d=[json.loads(x) for x in open(sys.argv[1]) if x.startswith('{')][-1]; v=d.get('gpu_ms_per_collect'); u=d.get('ppo_update') or {}; print(sys.argv[2], round((v if v is not None else d['ms_per_step'])*1e3, 2), 'us per', 'collect' if v is not None else 'step', '| ppo us per minibatch', round(u.get('fused_ms_per_minibatch', 0)*1e3, 2))" "$OUT/$tag.json" "$tag" | tee -a "$OUT/summary.txt"
 }
 for n in $NAMES; do chk "$n"; done
 for rep in 1 2; do
   for n in $NAMES; do
-    if [ "$MODE" = rollout ]; then run "$n" "$rep"; else run "$n" "$rep" 65536 && run "$n" "$rep" 524288; fi
+    if [ "$MODE" = exact ]; then run "$n" "$rep" 65536 && run "$n" "$rep" 524288; else run "$n" "$rep"; fi
   done
 done
