@@ -77,10 +77,11 @@ def parse(argv=None):
                     help="skip the wall-clock legs through the Python boundary (RocketVecEnv.step with host and "
                          "device outputs, the single-env gym Rocket6DOF.step)")
     ap.add_argument("--sb3-steps", type=int, default=100)
-    ap.add_argument("--n-sweep", default="4096,524288",
-                    help="other envs-per-GPU points of the north star's N in {4k, 64k, 512k}, timed with the same "
-                         "protocol (K steps after W warm-up, max over ranks) and reported in the line's n_sweep "
-                         "(empty: none)")
+    ap.add_argument("--n-sweep", default="4096,524288,4194304",
+                    help="other envs-per-GPU points of the north star's N in {4k, 64k, 512k}, plus 4M (a ~1 GB "
+                         "working set, 4x the 256 MB MALL: the true-HBM reading SURVEY.md 8d asks for), timed with "
+                         "the same protocol (K steps after W warm-up, max over ranks) and reported in the line's "
+                         "n_sweep (empty: none)")
     ap.add_argument("--mode", default="step", choices=["step", "rollout"],
                     help="step: the fused env step (headline); rollout: on-device PPO rollout "
                          "collection (MlpPolicy 64x64 forward + sample + env step + buffer), BASELINE configs[4]")
