@@ -40,6 +40,9 @@ POOL = 8
 # replays from here on (crossover of the ~8 us per-replay preamble against ~0.3 us per direct
 # launch, measured at N = 65536: DESIGN.md section 5)
 AUTO_LOOP_MAX_K = 32
+# warm-up of the n_sweep points: past the first episode ends, so that their K steps include the
+# done path (terminal rows, auto-reset) at its steady rate
+SWEEP_MIN_WARMUP = 100
 REFERENCE_PY_STEP = {"6DOF": 569, "3DOF": 3396}  # SURVEY.md §6, survey container, 1 core
 
 
@@ -1092,10 +1095,15 @@ def main():
             g_i = torch.Generator(device=dev)
             g_i.manual_seed(42 + rank)
             p_i = torch.rand((POOL, n_i, e_i.action_dim), device=dev, generator=g_i) * 2 - 1
-            r_i = timed_region(args, e_i, p_i, dev, dist, backend, launch)
+            # steady state: the timed steps come after the first episode ends (from step ~30 on,
+            # ~1.5 % of the envs end an episode per step; tools/phase_probe.py). Before them no lane
+            # takes the done path, which at N >= 524 288 costs 5-25 % (terminal rows, auto-reset)
+            a_i = argparse.Namespace(**vars(args))
+            a_i.warmup = max(args.warmup, SWEEP_MIN_WARMUP)
+            r_i = timed_region(a_i, e_i, p_i, dev, dist, backend, launch)
             b_i = bytes_env * n_i
             result["n_sweep"].append({
-                "envs_per_gpu": n_i, "global_envs": n_i * world, "value": n_i * world * K / r_i["dt"],
+                "envs_per_gpu": n_i, "warmup": a_i.warmup, "global_envs": n_i * world, "value": n_i * world * K / r_i["dt"],
                 "ms_per_step": r_i["dt"] / K * 1e3, "kernel_us": r_i["kern_ms"] * 1e3,
                 "frac": b_i / (r_i["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "frac_wall": b_i / (r_i["dt"] / K) / 1e9 / HBM_PEAK_GBS})

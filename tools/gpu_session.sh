@@ -42,7 +42,9 @@ if has prof; then
   # the driver's command under rocprofv3 --kernel-trace --stats (K = 20, N = 65536 and the sweep N)
   for N in 65536 524288 4194304; do
     mkdir -p "$OUT/rp_k20_n$N"
-    (cd /tmp && step rp_n$N 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rp_k20_n$N" -o bench -- python "$R/bench.py" --n $N --steps 20 --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$OUT/rp_k20_n$N/bench.json" 2> "$OUT/rp_k20_n$N/bench.err") || exit $?
+    # the sweep points at their steady state (bench.py SWEEP_MIN_WARMUP), the headline N as the driver runs it
+    W=5; [ "$N" -gt 65536 ] && W=100
+    (cd /tmp && step rp_n$N 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rp_k20_n$N" -o bench -- python "$R/bench.py" --n $N --steps 20 --warmup $W --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$OUT/rp_k20_n$N/bench.json" 2> "$OUT/rp_k20_n$N/bench.err") || exit $?
     python tools/rocprof_step.py "$OUT/rp_k20_n$N" --out "$OUT/rocprof_step_k20_n$N.json" > /dev/null
   done
 fi
