@@ -52,6 +52,11 @@ constexpr int kStAuxHelp = 16;
 // N = 65536: 5.49 -> 5.18 us; the same bit on the state planes, which the next launch re-reads,
 // is slower; nt loads +5 %).
 constexpr int kOutAux = 16;
+// terminal rows (the done lanes' scattered 56 + 4 + 4 B) of the plain kernels (N > kHelpMaxN):
+// nt. Past the MALL their partial lines cost ~24 us of a 200 us step at 4M envs in steady
+// state (~1.5 % of the envs done per step); nt: 197.5 -> 182.4 us at 4M, 19.4 -> 19.2 at 524288
+// (sc1: 200.5 / 18.8, sc1 | nt: 200.2 / 24.8; profiles/r04/phase/done_path_ab.txt)
+constexpr int kTermAuxLarge = 2;
 // largest N stepped with helper waves (step_kernel<..., HELP = true>); RR_HELP_MAX_N in the
 // environment overrides it at rr_create (tests select the plain kernel at small N with it)
 constexpr int64_t kHelpMaxN = 131072;
@@ -1009,8 +1014,8 @@ struct CounterLayout {
 
 // terminal obs / return / length of a done env (info["terminal_observation"], Monitor):
 // row i of [N][NS] as 16-B stores (rows are 4-B aligned; gfx950 buffer stores need only
-// dword alignment), NS = 14 -> 3 x 16 B + 8 B, NS = 7 -> 16 B + 12 B
-template <int NS>
+// dword alignment), NS = 14 -> 3 x 16 B + 8 B, NS = 7 -> 16 B + 12 B. AUX: cache policy
+template <int NS, int AUX>
 __device__ __forceinline__ void store_terminal(const Bufs& B, uint32_t i, uint32_t vo, uint32_t plane, const float* o,
                                                float ret, int32_t el)
 {
@@ -1021,16 +1026,16 @@ __device__ __forceinline__ void store_terminal(const Bufs& B, uint32_t i, uint32
                      __float_as_uint(o[j + 3])};
     };
 #pragma unroll
-    for (int j = 0; j + 4 <= NS; j += 4) __builtin_amdgcn_raw_buffer_store_b128(u4(j), tr, (int)(ro + j * 4), 0, 0);
+    for (int j = 0; j + 4 <= NS; j += 4) __builtin_amdgcn_raw_buffer_store_b128(u4(j), tr, (int)(ro + j * 4), 0, AUX);
     if constexpr (NS % 4 == 2)
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
-                                              (int)(ro + (NS - 2) * 4), 0, 0);
+                                              (int)(ro + (NS - 2) * 4), 0, AUX);
     else if constexpr (NS % 4 == 3)
         __builtin_amdgcn_raw_buffer_store_b96(
             u32x3{__float_as_uint(o[NS - 3]), __float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
-            (int)(ro + (NS - 3) * 4), 0, 0);
-    bst_f<0>(make_rsrc(B.term_ret, plane), ret, vo, 0);
-    bst_u<0>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
+            (int)(ro + (NS - 3) * 4), 0, AUX);
+    bst_f<AUX>(make_rsrc(B.term_ret, plane), ret, vo, 0);
+    bst_u<AUX>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
 }
 
 // per-env step outputs owned by the caller: reward, done (unless they travel in the obs row),
@@ -1174,7 +1179,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     const uint64_t m = __ballot(dv);
     if (lane == 0) B.done_bits[wave_idx] = m;
     if (m) {
-        if (dv) store_terminal<NS>(B, i, vo, plane, o, ret, el);
+        if (dv) store_terminal<NS, HELP ? 0 : kTermAuxLarge>(B, i, vo, plane, o, ret, el);
         if ((mode & RR_FLAG_AUTO_RESET) && dv) {
             if constexpr (HELP) {
                 while (__hip_atomic_load(&cflag[wv], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
