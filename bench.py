@@ -453,7 +453,7 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
         stored_rollout_rocprof(model, n, T, args.policy_dtype)
     if rp is not None and not args.rollout_torch and ro.one_launch and not ro.per_step:
         roof.update(achieved=flop / (rp["mean_ns"] * 1e-9) / 1e12, rocprof_mean_us=rp["mean_ns"] / 1e3,
-                    rocprof_source=rp_src)
+                    rocprof_source=rp_src, rocprof_median_of=rp.get("median_of"))
         roof["frac"] = roof["achieved"] / peak
         roof["frac_source"] = "rocprof"
     else:
@@ -836,24 +836,32 @@ def _isa_hashes():
     return _ISA
 
 
-def _stored(pattern, model, n):
-    """The newest committed profile file matching `pattern` for this kernel and N whose kernel
-    machine code (isa_hash of its kernel_name) is the code this process runs; else (None, reason)."""
+def _stored(pattern, model, n, key):
+    """The committed profile files matching `pattern` for this kernel and N whose kernel machine
+    code (isa_hash of its kernel_name) is the code this process runs: the median one by `key`
+    (re-measurements of the same code on other boxes scatter by a few %; no pick of the best),
+    with every matching path; else (None, reason)."""
     import glob
 
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", pattern % n), recursive=True),
-                  key=os.path.getmtime)
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", pattern % n), recursive=True))
     isa = _isa_hashes()
-    stale = None
-    for path in reversed(hits):
+    stale, match = None, []
+    for path in hits:
         with open(path) as f:
             d = json.load(f)
         if not d.get("kernel", "").startswith("step_kernel<%d," % model):
             continue
         if d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]:
-            return d, os.path.relpath(path, ROOT)
-        stale = stale or os.path.relpath(path, ROOT)
-    return None, ("no file measured on this kernel's machine code (latest, other code: %s)%s"
+            match.append((d[key], os.path.relpath(path, ROOT), d))
+        else:
+            stale = stale or os.path.relpath(path, ROOT)
+    if match:
+        match.sort(key=lambda m: m[0])
+        v, src, d = match[len(match) // 2]  # the upper median: never the best of two
+        d = dict(d, median_of="%d files of this code: %s" % (len(match), ", ".join(
+            "%s %.6g" % (m[1], m[0]) for m in match)))
+        return d, src
+    return None, ("no file measured on this kernel's machine code (other code: %s)%s"
                   % (stale, "; " + isa["__error__"] if "__error__" in isa else ""))
 
 
@@ -861,7 +869,7 @@ def stored_traffic(model, n):
     """Per-launch HBM bytes of the same kernel/config from the latest committed rocprofv3 PMC
     passes (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), only if they were measured on
     THIS kernel's machine code (same ISA hash); else (None, reason)."""
-    d, src = _stored("pmc_traffic_n%d.json", model, n)
+    d, src = _stored("pmc_traffic_n%d.json", model, n, "traffic_bytes")
     return (d["traffic_bytes"], src) if d else (None, src)
 
 
@@ -869,25 +877,33 @@ def stored_rocprof(model, n, steps):
     """The step kernel's rocprofv3 kernel-trace mean of the same protocol (tools/rocprof_step.py:
     a --kernel-trace --stats run of this bench command, committed under profiles/), only if it
     was measured on THIS kernel's machine code; else (None, reason)."""
-    return _stored("rocprof_step_k%d_n%%d.json" % steps, model, n)
+    return _stored("rocprof_step_k%d_n%%d.json" % steps, model, n, "mean_ns")
 
 
 def stored_rollout_rocprof(model, n, T, dtype):
     """The collect kernel's committed rocprofv3 kernel-trace mean (tools/rocprof_step.py on a
-    `bench.py --mode rollout` run) measured on this kernel's machine code; else (None, reason)."""
+    `bench.py --mode rollout` run) measured on this kernel's machine code — the median one when
+    several boxes measured it; else (None, reason)."""
     import glob
 
     hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "rocprof_rollout_n%d_t%d_%s.json" % (n, T, dtype)),
-                         recursive=True), key=os.path.getmtime)
+                         recursive=True))
     isa = _isa_hashes()
-    stale = None
-    for path in reversed(hits):
+    stale, match = None, []
+    for path in hits:
         with open(path) as f:
             d = json.load(f)
         if d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]:
-            return d, os.path.relpath(path, ROOT)
-        stale = stale or os.path.relpath(path, ROOT)
-    return None, "no collect-kernel trace measured on this machine code (latest, other code: %s)" % stale
+            match.append((d["mean_ns"], os.path.relpath(path, ROOT), d))
+        else:
+            stale = stale or os.path.relpath(path, ROOT)
+    if match:
+        match.sort(key=lambda m: m[0])
+        v, src, d = match[len(match) // 2]  # the upper median: never the best of two
+        d = dict(d, median_of="%d files of this code: %s" % (len(match), ", ".join(
+            "%s %.6g" % (m[1], m[0]) for m in match)))
+        return d, src
+    return None, "no collect-kernel trace measured on this machine code (other code: %s)" % stale
 
 
 def gather_leg_result(args, env, pool, dev, dist, backend, launch, n, world, K):
@@ -1003,7 +1019,8 @@ def main():
     rocprof = None
     if rp is not None:
         rocprof = {"mean_us": rp["mean_ns"] / 1e3, "frac": bytes_launch / (rp["mean_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS,
-                   "calls": rp["calls"], "events_us_same_run": rp.get("events_kernel_us"), "source": rp_src}
+                   "calls": rp["calls"], "events_us_same_run": rp.get("events_kernel_us"), "source": rp_src,
+                   "median_of": rp.get("median_of")}
     # `frac` is the profile-evidenced figure where a committed rocprofv3 kernel trace of this
     # command on this kernel's machine code exists (one GPU only: a stored 1-GPU trace does not
     # describe the ranks of a multi-GPU run), the live HIP-event figure otherwise
