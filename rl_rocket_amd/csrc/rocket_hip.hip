@@ -52,10 +52,13 @@ constexpr int kStAuxHelp = 16;
 // N = 65536: 5.49 -> 5.18 us; the same bit on the state planes, which the next launch re-reads,
 // is slower; nt loads +5 %).
 constexpr int kOutAux = 16;
-// terminal rows (the done lanes' scattered 56 + 4 + 4 B) of the plain kernels (N > kHelpMaxN):
-// nt. Past the MALL their partial lines cost ~24 us of a 200 us step at 4M envs in steady
-// state (~1.5 % of the envs done per step); nt: 197.5 -> 182.4 us at 4M, 19.4 -> 19.2 at 524288
-// (sc1: 200.5 / 18.8, sc1 | nt: 200.2 / 24.8; profiles/r04/phase/done_path_ab.txt)
+// terminal obs rows (the done lanes' scattered 56 B) of the plain kernels (N > kHelpMaxN): nt.
+// Past the MALL, 4-B stores from a few lanes of a wave cost far more than their bytes (one
+// partial line each): at 4M envs in steady state (~1.5 % of the envs done per step) the
+// terminal rows took ~24 us and the reset v0 ~20 us of a 200 us step. The rows go nt
+// (197.5 -> 182.4 us; sc1 200.5, sc1 | nt 200.2); the terminal return / length and v0 are stored
+// by every lane of a wave with a done lane, as whole lines (v0: 174.3 -> 157.3 us with the rows
+// off; profiles/r04/phase/done_path_ab.txt)
 constexpr int kTermAuxLarge = 2;
 // largest N stepped with helper waves (step_kernel<..., HELP = true>); RR_HELP_MAX_N in the
 // environment overrides it at rr_create (tests select the plain kernel at small N with it)
@@ -1015,7 +1018,7 @@ struct CounterLayout {
 // terminal obs / return / length of a done env (info["terminal_observation"], Monitor):
 // row i of [N][NS] as 16-B stores (rows are 4-B aligned; gfx950 buffer stores need only
 // dword alignment), NS = 14 -> 3 x 16 B + 8 B, NS = 7 -> 16 B + 12 B. AUX: cache policy
-template <int NS, int AUX>
+template <int NS, int AUX, bool SCALARS = true>
 __device__ __forceinline__ void store_terminal(const Bufs& B, uint32_t i, uint32_t vo, uint32_t plane, const float* o,
                                                float ret, int32_t el)
 {
@@ -1034,8 +1037,10 @@ __device__ __forceinline__ void store_terminal(const Bufs& B, uint32_t i, uint32
         __builtin_amdgcn_raw_buffer_store_b96(
             u32x3{__float_as_uint(o[NS - 3]), __float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, tr,
             (int)(ro + (NS - 3) * 4), 0, AUX);
-    bst_f<AUX>(make_rsrc(B.term_ret, plane), ret, vo, 0);
-    bst_u<AUX>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
+    if constexpr (SCALARS) {
+        bst_f<AUX>(make_rsrc(B.term_ret, plane), ret, vo, 0);
+        bst_u<AUX>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
+    }
 }
 
 // per-env step outputs owned by the caller: reward, done (unless they travel in the obs row),
@@ -1179,7 +1184,16 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     const uint64_t m = __ballot(dv);
     if (lane == 0) B.done_bits[wave_idx] = m;
     if (m) {
-        if (dv) store_terminal<NS, HELP ? 0 : kTermAuxLarge>(B, i, vo, plane, o, ret, el);
+        // plain kernels: the 4-B terminal return / length and the reset v0 leave as whole lines,
+        // from every lane of a wave with a done lane (the others' values are not read: terminal
+        // rows count at done indices only; v0 unchanged), below
+        if (dv) store_terminal<NS, HELP ? 0 : kTermAuxLarge, HELP>(B, i, vo, plane, o, ret, el);
+        if constexpr (!HELP) {
+            if (valid) {
+                bst_f<0>(make_rsrc(B.term_ret, plane), ret, vo, 0);
+                bst_u<0>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
+            }
+        }
         if ((mode & RR_FLAG_AUTO_RESET) && dv) {
             if constexpr (HELP) {
                 while (__hip_atomic_load(&cflag[wv], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
@@ -1193,11 +1207,14 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
                 for (int j = 0; j < NS; ++j) y1[j] = ic_s[j];
                 v0 = ic_v0;
             }
-            bst_f<SA>(st_r, v0, vo, v0_off);
+            if constexpr (HELP) bst_f<SA>(st_r, v0, vo, v0_off);
             cw = CL.next_episode(cw);
             normalize_obs<NS>(y1, H.inv_norm, o);
             el = 0;
             ret = 0.0f;
+        }
+        if constexpr (!HELP) {
+            if ((mode & RR_FLAG_AUTO_RESET) && valid) bst_f<SA>(st_r, v0, vo, v0_off);
         }
     }
     cw = CL.with_elapsed(cw, el);
