@@ -57,8 +57,8 @@ constexpr int kOutAux = 16;
 // partial line each): at 4M envs in steady state (~1.5 % of the envs done per step) the
 // terminal rows took ~24 us and the reset v0 ~20 us of a 200 us step. The rows go nt
 // (197.5 -> 182.4 us; sc1 200.5, sc1 | nt 200.2); the terminal return / length and v0 are stored
-// by every lane of a wave with a done lane, as whole lines (v0: 174.3 -> 157.3 us with the rows
-// off; profiles/r04/phase/done_path_ab.txt)
+// by every lane of a wave with a done lane, as whole lines, past the MALL (kModeWholeLines; v0:
+// 174.3 -> 157.3 us with the rows off; profiles/r04/phase/done_path_ab.txt)
 constexpr int kTermAuxLarge = 2;
 // largest N stepped with helper waves (step_kernel<..., HELP = true>); RR_HELP_MAX_N in the
 // environment overrides it at rr_create (tests select the plain kernel at small N with it)
@@ -102,8 +102,14 @@ constexpr float kTwoPi = 6.28318530717958648f;
 // reference's TimeLimit 800: 2^22 episodes per env before the episode field wraps), 16 without
 // a TimeLimit (KParams.el_mask / ep_shift, counter_bits()).
 constexpr int32_t kMaxEpisodeSteps = 0xFFFF;
-// step_kernel `mode` word: rr_params.flags plus "the counter word is live"
+// step_kernel `mode` word: rr_params.flags plus "the counter word is live" and "the batch is
+// past the MALL" (N > kWholeLineMinN: the done path's 4-B scalars leave as whole lines)
 constexpr uint32_t kModeCounter = 0x80000000u;
+constexpr uint32_t kModeWholeLines = 0x40000000u;
+// ~200 B of state, action and outputs per env and step: above ~1M envs a step's working set
+// passes the 256 MB MALL and partial lines become DRAM read-modify-writes (at 524 288, inside
+// it, the whole-line stores measured 2-4 % slower; at 4 194 304 10 % faster)
+constexpr int64_t kWholeLineMinN = 1 << 20;
 
 // Device-side constants, derived once on the host from rr_params (see make_kparams).
 struct KParams {
@@ -1184,12 +1190,12 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     const uint64_t m = __ballot(dv);
     if (lane == 0) B.done_bits[wave_idx] = m;
     if (m) {
-        // plain kernels: the 4-B terminal return / length and the reset v0 leave as whole lines,
-        // from every lane of a wave with a done lane (the others' values are not read: terminal
-        // rows count at done indices only; v0 unchanged), below
+        // plain kernels past the MALL: the 4-B terminal return / length and the reset v0 leave as
+        // whole lines, from every lane of a wave with a done lane (the others' values are not
+        // read: terminal rows count at done indices only; their v0 is unchanged)
         if (dv) store_terminal<NS, HELP ? 0 : kTermAuxLarge, HELP>(B, i, vo, plane, o, ret, el);
         if constexpr (!HELP) {
-            if (valid) {
+            if ((mode & kModeWholeLines) ? valid : dv) {
                 bst_f<0>(make_rsrc(B.term_ret, plane), ret, vo, 0);
                 bst_u<0>(make_rsrc(B.term_len, plane), (uint32_t)el, vo, 0);
             }
@@ -1207,14 +1213,14 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
                 for (int j = 0; j < NS; ++j) y1[j] = ic_s[j];
                 v0 = ic_v0;
             }
-            if constexpr (HELP) bst_f<SA>(st_r, v0, vo, v0_off);
+            if (HELP || !(mode & kModeWholeLines)) bst_f<SA>(st_r, v0, vo, v0_off);
             cw = CL.next_episode(cw);
             normalize_obs<NS>(y1, H.inv_norm, o);
             el = 0;
             ret = 0.0f;
         }
         if constexpr (!HELP) {
-            if ((mode & RR_FLAG_AUTO_RESET) && valid) bst_f<SA>(st_r, v0, vo, v0_off);
+            if ((mode & kModeWholeLines) && (mode & RR_FLAG_AUTO_RESET) && valid) bst_f<SA>(st_r, v0, vo, v0_off);
         }
     }
     cw = CL.with_elapsed(cw, el);
@@ -1646,6 +1652,10 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     if (p->max_episode_steps < 0 || p->max_episode_steps > kMaxEpisodeSteps)
         return fail(RR_EINVAL, "rr_create: max_episode_steps must be in [0, 65535]");
     if (!(p->dt > 0.0)) return fail(RR_EINVAL, "rr_create: dt must be > 0");
+    constexpr uint32_t kKnownFlags = RR_FLAG_AUTO_RESET | RR_FLAG_EPISODE_STATS | RR_FLAG_REWARD_ANNEALING |
+                                     RR_FLAG_ACTION_SOA | RR_FLAG_SCIPY_H0_CLAMP | RR_FLAG_HOST_STATE;
+    if (p->flags & ~kKnownFlags)  // the high bits carry the kernels' internal mode (kModeCounter, ...)
+        return fail(RR_EINVAL, "rr_create: unknown flag bits");
     rr_env* e = new (std::nothrow) rr_env();
     if (!e) return fail(RR_ENOMEM, "rr_create: host allocation failed");
     e->device = device;
@@ -1829,7 +1839,8 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     } else {
         const uint32_t nn = (uint32_t)e->n;
         const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
-        const uint32_t mode = e->p.flags | (counter ? kModeCounter : 0u);
+        const uint32_t mode =
+            e->p.flags | (counter ? kModeCounter : 0u) | (e->n > kWholeLineMinN ? kModeWholeLines : 0u);
         const bool soa = e->p.flags & RR_FLAG_ACTION_SOA;
         // small N (at most ~2 main waves per SIMD): helper waves draw the reset candidates
         const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;

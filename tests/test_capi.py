@@ -48,6 +48,11 @@ def test_invalid_arguments_fail_cleanly_without_gpu():
     assert lib.rr_create(ctypes.byref(h), ctypes.byref(p), 16, 0, 0) == _lib.RR_EINVAL
     p.max_episode_steps = 800
     assert lib.rr_create(ctypes.byref(h), ctypes.byref(p), 0, 0, 0) == _lib.RR_EINVAL
+    for bad in (0x40, 0x40000000, 0x80000000):  # the high bits are the kernels' internal mode word
+        p.flags = 0x1 | bad
+        assert lib.rr_create(ctypes.byref(h), ctypes.byref(p), 16, 0, 0) == _lib.RR_EINVAL
+        assert b"flag" in lib.rr_last_error()
+    p.flags = 0x1
     assert lib.rr_step(None, None, None, None, None, None, None, None) == _lib.RR_EINVAL
     assert lib.rr_destroy(None) == 0
     assert lib.rr_num_envs(None) == -1
