@@ -880,6 +880,28 @@ def stored_rocprof(model, n, steps):
     return _stored("rocprof_step_k%d_n%%d.json" % steps, model, n, "mean_ns")
 
 
+def stored_exact_fp64(n):
+    """fp64 VALU issue rate of the exact-mode kernel at this N (profiles/**/exact_counters_n<N>.json
+    measured on the machine code this process runs): the upper median of the matching files."""
+    import glob
+
+    isa = _isa_hashes()
+    match = []
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "exact_counters_n%d.json" % n),
+                                 recursive=True)):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("fp64") and d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]:
+            match.append((d["fp64"]["achieved_tflops"], os.path.relpath(path, ROOT), d))
+    if not match:
+        return {"source": "no exact-mode counters of this machine code at N = %d" % n}
+    match.sort(key=lambda m: m[0])
+    v, src, d = match[len(match) // 2]
+    return {"bound": "fp64 VALU", "achieved": v, "peak": d["fp64"]["peak_tflops"], "unit": "TFLOP/s",
+            "frac": d["fp64"]["frac"], "kernel_us": d["kernel_trace"]["mean_us"], "kernel": d["kernel_name"],
+            "what": d["fp64"]["what"], "source": src}
+
+
 def stored_rollout_rocprof(model, n, T, dtype):
     """The collect kernel's committed rocprofv3 kernel-trace mean (tools/rocprof_step.py on a
     `bench.py --mode rollout` run) measured on this kernel's machine code — the median one when
@@ -1089,6 +1111,11 @@ def main():
                      "bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": bytes_env},
     }
+
+    if args.integrator == "dopri5" and world == 1:
+        # the exact mode is fp64 VALU work, not HBM-bound: its issue rate against the fp64 vector
+        # peak from the committed counters of the same N and machine code (tools/exact_counters.py)
+        result["roofline_fp64"] = stored_exact_fp64(n)
 
     # ---- the step + all_gather leg (reported separately from the step alone) ----
     if launch == "isolated":

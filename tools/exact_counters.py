@@ -12,6 +12,7 @@ import glob
 import json
 import os
 import statistics
+import sys
 
 
 def counters(d, grid=None):
@@ -69,6 +70,23 @@ def main():
         if "SQ_INSTS_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
             d["valu_cycles_per_valu_inst"] = 4 * c["SQ_ACTIVE_INST_VALU"] / c["SQ_INSTS_VALU"]
         res["derived"] = d
+    # fp64 VALU FLOPs issued per dispatch (64 lanes per wave-instruction, masked lanes included: an
+    # upper bound of the useful work) over the kernel-trace mean at the same N, against the fp64
+    # vector peak (MI355X_MICROARCH.md: 78.6 TF)
+    if all(k in c for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64")) and \
+            "kernel_trace" in res:
+        fl = 64 * (c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + 2 * c["SQ_INSTS_VALU_FMA_F64"])
+        t = res["kernel_trace"]["mean_us"] * 1e-6
+        res["fp64"] = {"flops_per_dispatch": fl, "achieved_tflops": fl / t / 1e12, "peak_tflops": 78.6,
+                       "frac": fl / t / 1e12 / 78.6,
+                       "what": "64 x (ADD_F64 + MUL_F64 + 2 FMA_F64) wave-instructions per dispatch over the "
+                               "kernel-trace mean (masked lanes counted: issue rate, not useful work)"}
+    if "kernel_trace" in res:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from rl_rocket_amd.build import kernel_isa_hashes
+
+        res["kernel_name"] = res["kernel_trace"]["name"]
+        res["isa_hash"] = kernel_isa_hashes().get(res["kernel_name"])
     res["source"] = a.run_dir
     text = json.dumps(res, indent=1)
     print(text)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session of the round (phases in one gpurun call). Every GPU step has its own timeout;
 # a crash / timeout / abort ends the script (exit codes other than 0 / 1 stop it).
-#   tools/gpu_session.sh TAG "PHASES"   PHASES: any of tests bench dist prof pmc rollout legs floor exact
+#   tools/gpu_session.sh TAG "PHASES"   PHASES: any of tests bench dist prof pmc rollout legs floor exact exactpmc
 #   (default: tests bench prof pmc rollout)
 TAG=${1:-run}
 PHASES=${2:-"tests bench prof pmc rollout"}
@@ -92,6 +92,20 @@ if has exact; then
   for N in 65536 524288; do
     mkdir -p "$OUT/exact_kt_n$N"
     (cd /tmp && step exact_kt_n$N 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/exact_kt_n$N" -o bench -- python "$R/bench.py" --integrator dopri5 --n $N --steps 50 --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$OUT/exact_kt_n$N/bench.json" 2>&1) || exit $?
+  done
+fi
+if has exactpmc; then
+  # the exact kernels' fp64 VALU counters at N = 65 536 (in-loop kernel) and 524 288 (lean kernel):
+  # tools/exact_counters.py -> achieved fp64 FLOP/s against the 78.6 TF vector peak
+  for N in 65536 524288; do
+    D="$OUT/exactpmc_n$N"; mkdir -p "$D"
+    step exactpmc_bench_n$N 300 $B --integrator dopri5 --n $N --steps 50 --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$D/bench_exact.json" 2> "$D/bench_exact.err"
+    cd /tmp || exit 2
+    step exactpmc_kt_n$N 300 rocprofv3 --kernel-trace --output-format csv -d "$D/exact_kt" -o kt -- python "$R/bench.py" --integrator dopri5 --n $N --steps 50 --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$D/exact_kt.log" 2>&1
+    step exactpmc_sq_n$N 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$D/exact_SQ" -o pmc -- python "$R/bench.py" --integrator dopri5 --n $N --steps 20 --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$D/exact_SQ.log" 2>&1
+    step exactpmc_sq2_n$N 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$D/exact_SQ2" -o pmc -- python "$R/bench.py" --integrator dopri5 --n $N --steps 20 --warmup 5 --no-cpu-baseline --no-sb3-legs --n-sweep "" > "$D/exact_SQ2.log" 2>&1
+    cd "$R" || exit 2
+    python tools/exact_counters.py "$D" --out "$OUT/exact_counters_n$N.json" > /dev/null
   done
 fi
 echo done
