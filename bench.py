@@ -836,20 +836,21 @@ def _isa_hashes():
     return _ISA
 
 
-def _stored(pattern, model, n, key):
+def _stored(pattern, model, n, key, kernel_prefix=None):
     """The committed profile files matching `pattern` for this kernel and N whose kernel machine
-    code (isa_hash of its kernel_name) is the code this process runs: the median one by `key`
-    (re-measurements of the same code on other boxes scatter by a few %; no pick of the best),
-    with every matching path; else (None, reason)."""
+    code (isa_hash of its kernel_name) is the code this process runs: the upper median one by
+    `key` (re-measurements of the same code on other boxes scatter by a few %; never the best of
+    two), with the matching files listed under `median_of`; else (None, reason)."""
     import glob
 
+    prefix = kernel_prefix or ("step_kernel<%d," % model)
     hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", pattern % n), recursive=True))
     isa = _isa_hashes()
     stale, match = None, []
     for path in hits:
         with open(path) as f:
             d = json.load(f)
-        if not d.get("kernel", "").startswith("step_kernel<%d," % model):
+        if not d.get("kernel", "").startswith(prefix):
             continue
         if d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]:
             match.append((d[key], os.path.relpath(path, ROOT), d))
@@ -857,7 +858,7 @@ def _stored(pattern, model, n, key):
             stale = stale or os.path.relpath(path, ROOT)
     if match:
         match.sort(key=lambda m: m[0])
-        v, src, d = match[len(match) // 2]  # the upper median: never the best of two
+        v, src, d = match[len(match) // 2]
         d = dict(d, median_of="%d files of this code: %s" % (len(match), ", ".join(
             "%s %.6g" % (m[1], m[0]) for m in match)))
         return d, src
@@ -904,28 +905,9 @@ def stored_exact_fp64(n):
 
 def stored_rollout_rocprof(model, n, T, dtype):
     """The collect kernel's committed rocprofv3 kernel-trace mean (tools/rocprof_step.py on a
-    `bench.py --mode rollout` run) measured on this kernel's machine code — the median one when
-    several boxes measured it; else (None, reason)."""
-    import glob
-
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "rocprof_rollout_n%d_t%d_%s.json" % (n, T, dtype)),
-                         recursive=True))
-    isa = _isa_hashes()
-    stale, match = None, []
-    for path in hits:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]:
-            match.append((d["mean_ns"], os.path.relpath(path, ROOT), d))
-        else:
-            stale = stale or os.path.relpath(path, ROOT)
-    if match:
-        match.sort(key=lambda m: m[0])
-        v, src, d = match[len(match) // 2]  # the upper median: never the best of two
-        d = dict(d, median_of="%d files of this code: %s" % (len(match), ", ".join(
-            "%s %.6g" % (m[1], m[0]) for m in match)))
-        return d, src
-    return None, "no collect-kernel trace measured on this machine code (other code: %s)" % stale
+    `bench.py --mode rollout` run) measured on this kernel's machine code; else (None, reason)."""
+    return _stored("rocprof_rollout_n%%d_t%d_%s.json" % (T, dtype), model, n, "mean_ns",
+                   kernel_prefix="rollout_step_kernel<%d," % model)
 
 
 def gather_leg_result(args, env, pool, dev, dist, backend, launch, n, world, K):
