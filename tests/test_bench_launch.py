@@ -126,3 +126,27 @@ def test_rollout_roofline_counts():
     b16 = bench.rollout_bytes_per_env_step(14, 3, 16)
     assert bench.rollout_bytes_per_env_step(14, 3, 10 ** 9) == pytest.approx(92.0)
     assert 92.0 < b16 < 110.0
+
+
+def test_committed_traces_quote_the_upper_median_of_this_machine_code(tmp_path, monkeypatch):
+    """bench.py quotes, of the committed traces measured on the running kernel's machine code,
+    the upper median (re-runs on other boxes scatter; never the best of two) and lists them;
+    traces of other code are ignored."""
+    import json
+
+    import bench
+
+    name = "void step_kernel<6, 0, false, true, 4, false>(...)"
+    for tag, mean, isa in (("a", 4800.0, "h1"), ("b", 4300.0, "h1"), ("c", 4000.0, "old"), ("d", 4700.0, "h1")):
+        d = tmp_path / "profiles" / "r9" / tag
+        d.mkdir(parents=True)
+        (d / "rocprof_step_k20_n64.json").write_text(json.dumps(
+            {"kernel": "step_kernel<6,RK4>", "kernel_name": name, "isa_hash": isa, "mean_ns": mean}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "_isa_hashes", lambda: {name: "h1"})
+    d, src = bench.stored_rocprof(6, 64, 20)
+    assert d["mean_ns"] == 4700.0 and src.endswith("r9/d/rocprof_step_k20_n64.json")  # of 4300 / 4700 / 4800
+    assert d["median_of"].startswith("3 files")
+    monkeypatch.setattr(bench, "_isa_hashes", lambda: {name: "other"})
+    d, why = bench.stored_rocprof(6, 64, 20)
+    assert d is None and "no file" in why
