@@ -5,6 +5,9 @@
 #   tools/ab_libs.sh TAG rollout NAME...   rollout collect (--no-ppo), us per collect
 #   tools/ab_libs.sh TAG exact NAME...     exact mode at N = 65 536 and 524 288, ms per step
 #   tools/ab_libs.sh TAG ppo NAME...       fused PPO minibatch update (rollout bench with PPO), ms
+# The libraries are built beforehand, in this container, from edited copies of the sources, e.g.
+#   python -c "from rl_rocket_amd import build as B; B.build_lib(out='tools/ab/lib_x.so', extra=[...])"
+# (tools/ab/ is not committed; the A/B summaries go to profiles/rNN/ab_*/).
 TAG=${1:-ab}; MODE=${2:-rollout}; shift 2
 NAMES=${*:-"base"}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
