@@ -37,9 +37,10 @@ BYTES_PER_STEP = {6: 56 + 12 + 4 + 56 + 56 + 4 + 1, 3: 28 + 8 + 4 + 28 + 28 + 4 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 POOL = 8
 # --launch auto: direct launches (tools/libbench_timed.so) below this many timed steps, hipGraph
-# replays from here on (crossover of the ~8 us per-replay preamble against ~0.3 us per direct
-# launch, measured at N = 65536: DESIGN.md section 5)
-AUTO_LOOP_MAX_K = 32
+# replays from here on. Direct launches cost the host 3-4.8 us each against the kernel's ~4.2 us,
+# so a run of them is host-paced at times: K = 20 at N = 65536 measured 5.5-6.6 us per step by
+# the wall clock, one 20-launch graph replay 5.2-5.3 (round 4, profiles/r04/launch/)
+AUTO_LOOP_MAX_K = 8
 # warm-up of the n_sweep points: past the first episode ends, so that their K steps include the
 # done path (terminal rows, auto-reset) at its steady rate
 SWEEP_MIN_WARMUP = 100
