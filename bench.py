@@ -837,49 +837,71 @@ def _isa_hashes():
     return _ISA
 
 
-def _stored(pattern, model, n, key, kernel_prefix=None):
+def launch_kind(launch):
+    """'graph' / 'direct' / 'eager' of a bench line's config.launch string (or a stored trace's)."""
+    launch = (launch or "").strip()
+    if launch.startswith("graph"):
+        return "graph"
+    if launch.startswith("direct"):
+        return "direct"
+    return "eager"
+
+
+def _stored(pattern, model, n, key, kernel_prefix=None, launch=None, upper=True):
     """The committed profile files matching `pattern` for this kernel and N whose kernel machine
-    code (isa_hash of its kernel_name) is the code this process runs: the upper median one by
-    `key` (re-measurements of the same code on other boxes scatter by a few %; never the best of
-    two), with the matching files listed under `median_of`; else (None, reason)."""
+    code (isa_hash of its kernel_name) is the code this process runs — and, with `launch`
+    ('graph' / 'direct'), that were recorded with the same launch mode as the running command
+    (a trace of direct launches does not describe graph replays: the tracer's per-dispatch cost
+    differs). Of those, the median one by `key` in the conservative direction of that key
+    (upper=True: the upper median, for a duration; upper=False: the lower median, for a byte count
+    that would raise a bandwidth), never the best of two; the matching files are listed under
+    `median_of`, the selection under `selection`. Else (None, reason)."""
     import glob
 
     prefix = kernel_prefix or ("step_kernel<%d," % model)
     hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", pattern % n), recursive=True))
     isa = _isa_hashes()
-    stale, match = None, []
+    stale, other_launch, match = None, None, []
     for path in hits:
         with open(path) as f:
             d = json.load(f)
         if not d.get("kernel", "").startswith(prefix):
             continue
-        if d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]:
-            match.append((d[key], os.path.relpath(path, ROOT), d))
-        else:
+        if not (d.get("isa_hash") and isa.get(d.get("kernel_name")) == d["isa_hash"]):
             stale = stale or os.path.relpath(path, ROOT)
+        elif launch is not None and launch_kind(d.get("launch")) != launch:
+            other_launch = other_launch or os.path.relpath(path, ROOT)
+        else:
+            match.append((d[key], os.path.relpath(path, ROOT), d))
     if match:
         match.sort(key=lambda m: m[0])
-        v, src, d = match[len(match) // 2]
-        d = dict(d, median_of="%d files of this code: %s" % (len(match), ", ".join(
-            "%s %.6g" % (m[1], m[0]) for m in match)))
+        v, src, d = match[len(match) // 2 if upper else (len(match) - 1) // 2]
+        d = dict(d, median_of="%d files of this code%s: %s" % (
+            len(match), "" if launch is None else " and launch mode (%s)" % launch,
+            ", ".join("%s %.6g" % (m[1], m[0]) for m in match)),
+            selection="%s median by %s of the committed files of this machine code%s" % (
+                "upper" if upper else "lower", key, "" if launch is None else ", %s launches only" % launch))
         return d, src
-    return None, ("no file measured on this kernel's machine code (other code: %s)%s"
-                  % (stale, "; " + isa["__error__"] if "__error__" in isa else ""))
+    return None, ("no file measured on this kernel's machine code%s (other code: %s%s)%s"
+                  % ("" if launch is None else " with %s launches" % launch, stale,
+                     "" if other_launch is None else "; other launch mode: %s" % other_launch,
+                     "; " + isa["__error__"] if "__error__" in isa else ""))
 
 
 def stored_traffic(model, n):
     """Per-launch HBM bytes of the same kernel/config from the latest committed rocprofv3 PMC
     passes (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), only if they were measured on
-    THIS kernel's machine code (same ISA hash); else (None, reason)."""
-    d, src = _stored("pmc_traffic_n%d.json", model, n, "traffic_bytes")
+    THIS kernel's machine code (same ISA hash): the lower median; else (None, reason)."""
+    d, src = _stored("pmc_traffic_n%d.json", model, n, "traffic_bytes", upper=False)
     return (d["traffic_bytes"], src) if d else (None, src)
 
 
-def stored_rocprof(model, n, steps):
+def stored_rocprof(model, n, steps, launch=None):
     """The step kernel's rocprofv3 kernel-trace mean of the same protocol (tools/rocprof_step.py:
     a --kernel-trace --stats run of this bench command, committed under profiles/), only if it
-    was measured on THIS kernel's machine code; else (None, reason)."""
-    return _stored("rocprof_step_k%d_n%%d.json" % steps, model, n, "mean_ns")
+    was measured on THIS kernel's machine code and, with `launch`, with the same launch mode;
+    the upper median; else (None, reason)."""
+    return _stored("rocprof_step_k%d_n%%d.json" % steps, model, n, "mean_ns", launch=launch)
 
 
 def stored_exact_fp64(n):
@@ -1007,7 +1029,8 @@ def main():
     headline_cfg = not (args.monitor or args.allgather or args.integrator != "rk4" or launch == "isolated")
     if headline_cfg:
         traffic, traffic_src = stored_traffic(model, n)
-        rp, rp_src = stored_rocprof(model, n, K)
+        rp, rp_src = stored_rocprof(model, n, K, launch="graph" if reg["use_graph"] else
+                                    "direct" if reg["use_loop"] else "eager")
     else:
         traffic, traffic_src = None, "PMC traffic files cover the headline configuration (RK4, no Monitor, no gather)"
         rp, rp_src = None, "rocprofv3 files cover the headline configuration"
@@ -1025,7 +1048,7 @@ def main():
     if rp is not None:
         rocprof = {"mean_us": rp["mean_ns"] / 1e3, "frac": bytes_launch / (rp["mean_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS,
                    "calls": rp["calls"], "events_us_same_run": rp.get("events_kernel_us"), "source": rp_src,
-                   "median_of": rp.get("median_of")}
+                   "launch": rp.get("launch"), "median_of": rp.get("median_of"), "selection": rp.get("selection")}
     # `frac` is the profile-evidenced figure where a committed rocprofv3 kernel trace of this
     # command on this kernel's machine code exists (one GPU only: a stored 1-GPU trace does not
     # describe the ranks of a multi-GPU run), the live HIP-event figure otherwise
@@ -1035,7 +1058,16 @@ def main():
     frac_events = achieved / HBM_PEAK_GBS
     if rocprof is not None:
         achieved_line, frac_line = bytes_launch / (rp["mean_ns"] * 1e-9) / 1e9, rocprof["frac"]
-        frac_source = "rocprof: %s (mean kernel-trace duration of this command, %d dispatches)" % (rp_src, rp["calls"])
+        frac_source = "rocprof: %s (mean kernel-trace duration of this command, %d dispatches; %s)" % (
+            rp_src, rp["calls"], rp.get("selection"))
+        # the live HIP-event figure against the committed trace: the tracer adds its per-dispatch
+        # completion handling (~0.5 us at N = 65 536), so events normally read a few to
+        # ~15 % above it; outside [0.85, 1.30] the committed figure does not describe this run
+        ratio = frac_events / rocprof["frac"]
+        rocprof["events_over_rocprof"] = ratio
+        if not 0.85 <= ratio <= 1.30:
+            rocprof["warning"] = ("the live events figure (%.3f) and the committed rocprofv3 figure (%.3f) differ by "
+                                  "more than the tracer's overhead explains" % (frac_events, rocprof["frac"]))
     else:
         achieved_line, frac_line = achieved, frac_events
         frac_source = "events: HIP events on the launch stream around the K launches of this run" + \

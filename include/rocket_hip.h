@@ -146,6 +146,8 @@ int rr_action_dim(const rr_env* e);
  * in the order of `stream` (launches queued on it before the call read the old key) and the
  * call returns once it has landed (it synchronises `stream`, nothing else); it applies to every
  * launch that runs after it, including replays of hipGraphs captured before it, at every N.
+ * If the handle's last step / reset / rollout launch went to a DIFFERENT stream, the call first
+ * synchronises the device, so that no launch still queued there reads a half-written key.
  * RR_EINVAL while `stream` is being captured into a graph. */
 int rr_seed(rr_env* e, uint64_t seed, void* stream);
 /* Sample a fresh initial condition for every env where mask[i] != 0 (all when mask is

@@ -83,7 +83,13 @@ class RoCfg(ctypes.Structure):
         ("att_limit", ctypes.c_double * 3),
         ("land_att_limit", ctypes.c_double * 3),
         ("omega_lim", ctypes.c_double * 3),
+        ("integrator", ctypes.c_int32),
     ]
+
+
+# RoCfg.integrator (rocket_oracle.h): the reference's scipy RK45 step, or the build's explicit-Euler
+# speed mode (RR_INT_EULER, BASELINE.json configs[1])
+INTEGRATORS = {"rk45": 0, "euler": 1}
 
 
 def derived6(IC, ICRange, **_):
@@ -116,10 +122,11 @@ def derived3(IC, ICRange, **_):
     return norm, xb, zb, max_gimbal, max_thrust
 
 
-def make_cfg(model, scipy_clamp_h0=False, **kw):
+def make_cfg(model, scipy_clamp_h0=False, integrator="rk45", **kw):
     c = RoCfg()
     c.model = model
     c.scipy_clamp_h0 = int(scipy_clamp_h0)
+    c.integrator = INTEGRATORS[integrator]
     c.dt = float(kw.get("timestep", 0.1))
     rc = kw["reward_coeff"]
     norm = np.zeros(14)

@@ -420,6 +420,31 @@ static int solve_ivp_rk45(const ro_cfg* c, const ctrl* k, int n, int idx, double
     return status;
 }
 
+/* Explicit Euler step (RO_INT_EULER, rocket_oracle.h): one RHS evaluation (simulator.py:259-294 /
+ * :88-130), the terminal altitude event (the sign-change test of solve_ivp's find_active_events,
+ * ivp.py, as used at simulator.py:230-241 / :58-69) with its root on Euler's linear continuous
+ * extension, every component evaluated there. */
+static int euler_step(const ro_cfg* c, const ctrl* k, int n, int idx, const double* y0, double* y_out,
+                      int* nfev)
+{
+    double f0[NMAX];
+    rhs(k, y0, f0);
+    *nfev = 1;
+    for (int i = 0; i < n; ++i) y_out[i] = y0[i] + c->dt * f0[i];
+    const double g0 = y0[idx], g1 = y_out[idx];
+    int status = 0;
+    if ((g0 <= 0 && g1 >= 0) || (g0 >= 0 && g1 <= 0)) {
+        status = 1;
+        if (g1 != 0) { /* a root at the step end keeps y1 */
+            const double s = g0 / (g0 - g1);
+            for (int i = 0; i < n; ++i) y_out[i] = y0[i] + (s * c->dt) * f0[i];
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        if (!isfinite(y_out[i])) status = status ? status : -1;
+    return status;
+}
+
 /* ---------------------------------------------------------------------------
  * Env layer.
  * ------------------------------------------------------------------------- */
@@ -583,7 +608,8 @@ void ro_step(const ro_cfg* c, const float* ic, double t_in, const double* s_in, 
     const int idx = c->model == 6 ? 0 : 1;
     double y[NMAX];
     int nfev = 0;
-    int status = solve_ivp_rk45(c, &k, n, idx, t_in, s_in, y, &nfev);
+    int status = c->integrator == RO_INT_EULER ? euler_step(c, &k, n, idx, s_in, y, &nfev)
+                                               : solve_ivp_rk45(c, &k, n, idx, t_in, s_in, y, &nfev);
     if (c->model == 6) {
         /* _normalize_quaternion, simulator.py:250 */
         double nq = sqrt(y[6] * y[6] + y[7] * y[7] + y[8] * y[8] + y[9] * y[9]);

@@ -65,9 +65,10 @@ constexpr int kTermAuxLarge = 2;
 constexpr int64_t kHelpMaxN = 131072;
 // largest N stepped with one main wave per workgroup (helper variant)
 constexpr int64_t kNarrowMaxN = 16384;
-// largest N of the exact mode's one-wave-per-SIMD 6DOF kernel (256 CUs x 4 SIMDs x 64 lanes:
-// one env per lane); above it the lean two-waves-per-SIMD kernel (rocket_dopri5.inc, solve LEAN)
-constexpr int64_t kExactLeanMinN = 256 * 4 * 64;
+// exact mode: the one-wave-per-SIMD 6DOF kernel runs up to (CUs x 4 SIMDs x 64 lanes) envs, one
+// env per lane; above it the lean two-waves-per-SIMD kernel (rocket_dopri5.inc, solve LEAN). The
+// CU count is the device's (rr_create); kExactLeanCUs is the fallback if the query fails
+constexpr int64_t kExactLeanCUs = 256;
 constexpr int kWave = 64;
 constexpr int kBlock = 256;  // threads per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
@@ -108,7 +109,8 @@ constexpr uint32_t kModeCounter = 0x80000000u;
 constexpr uint32_t kModeWholeLines = 0x40000000u;
 // ~200 B of state, action and outputs per env and step: above ~1M envs a step's working set
 // passes the 256 MB MALL and partial lines become DRAM read-modify-writes (at 524 288, inside
-// it, the whole-line stores measured 2-4 % slower; at 4 194 304 10 % faster)
+// it, the whole-line stores measured 2-4 % slower; at 4 194 304 10 % faster). RR_WHOLE_LINE_MIN_N
+// in the environment overrides it at rr_create (tests run the whole-line path at small N)
 constexpr int64_t kWholeLineMinN = 1 << 20;
 
 // Device-side constants, derived once on the host from rr_params (see make_kparams).
@@ -684,8 +686,9 @@ __device__ __forceinline__ void integrate(const KParams& P, const Ctl& c, const 
 // (ivp.py handle_events, rk.py RkDenseOutput). Here the step's dense output is the
 // cubic Hermite interpolant through (y0, f(y0)) and (y1, f(y1)) — 4th-order like the
 // reference's — its altitude root is found by safeguarded Newton, and every state
-// component is evaluated there.
-template <int MODEL>
+// component is evaluated there. Explicit Euler (RR_INT_EULER) uses its own continuous extension,
+// the line y0 + s h f(y0): root s = x0 / (x0 - x1) (oracle/rocket_oracle.c euler_step).
+template <int MODEL, int INTEG>
 __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const float* y0, const float* f0,
                                            float* y1)
 {
@@ -693,6 +696,12 @@ __device__ __forceinline__ void event_step(const KParams& P, const Ctl& c, const
     constexpr int NS = Dims<MODEL>::NS;
     const float x0 = y0[EV], x1 = y1[EV];
     if (x1 == 0.0f) return;  // root at the step end: state unchanged
+    if constexpr (INTEG == RR_INT_EULER) {
+        const float sh = (x0 * frcp(x0 - x1)) * P.h;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) y1[j] = fmaf(sh, f0[j], y0[j]);
+        return;
+    }
     float f1[NS];
     if constexpr (MODEL == 6) rhs6_pk(c, y1, f1);
     else rhs<MODEL>(P, c, y1, f1);
@@ -980,7 +989,7 @@ __device__ __forceinline__ bool physics_step(const KParams& P, const float* a, c
     integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
     const float g0 = y0[EV], g1 = y1[EV];
     const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
-    if (event) event_step<MODEL>(P, c, y0, f0, y1);
+    if (event) event_step<MODEL, INTEG>(P, c, y0, f0, y1);
     post_integrate<MODEL>(y1);
     return event;
 }
@@ -1576,7 +1585,9 @@ struct rr_env {
     int64_t n, id_off;
     uint64_t steps;
     int64_t help_max_n;       // largest N stepped with helper waves (kHelpMaxN, RR_HELP_MAX_N env override)
-    int64_t exact_lean_min_n; // 6DOF exact mode: lean kernel above this N (kExactLeanMinN, RR_EXACT_LEAN_MIN_N)
+    int64_t exact_lean_min_n; // 6DOF exact mode: lean kernel above this N (CUs x 256, RR_EXACT_LEAN_MIN_N)
+    int64_t whole_line_min_n; // plain step kernels: whole-line done-path stores above this N (kWholeLineMinN,
+                              // RR_WHOLE_LINE_MIN_N)
     float* state;
     float* v0;
     uint32_t* counter;
@@ -1594,6 +1605,10 @@ struct rr_env {
     float* g_ret;
     int32_t* g_len;
     uint8_t* g_trunc;   // rr_gather_rows scratch
+    // the stream of the last launch that reads the reset-stream key (step, reset, rollout kernels):
+    // rr_seed on another stream first waits for the device (a stored handle, never dereferenced)
+    void* last_stream;
+    bool launched;
 };
 
 namespace {
@@ -1667,15 +1682,23 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->nt = p->model == RR_MODEL_6DOF ? 5 : 6;
     e->n = n;
     e->id_off = env_id_offset;
+    DeviceGuard g(device);
     {
         // test / A-B override of the helper-wave threshold: RR_HELP_MAX_N=<n> in the environment
         const char* hv = std::getenv("RR_HELP_MAX_N");
         e->help_max_n = hv ? std::strtoll(hv, nullptr, 10) : kHelpMaxN;
-        // the same for the exact mode's lean-kernel threshold (tests run the lean kernel at small N)
+        // the exact mode's lean-kernel threshold: one env per lane of one wave per SIMD of THIS
+        // device (a partitioned or smaller part has fewer CUs); RR_EXACT_LEAN_MIN_N overrides it
+        // (tests run the lean kernel at small N)
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+            cus = (int)kExactLeanCUs;
         const char* lv = std::getenv("RR_EXACT_LEAN_MIN_N");
-        e->exact_lean_min_n = lv ? std::strtoll(lv, nullptr, 10) : kExactLeanMinN;
+        e->exact_lean_min_n = lv ? std::strtoll(lv, nullptr, 10) : (int64_t)cus * 4 * kWave;
+        // the plain kernels' whole-line done path (tests run it at small N with RR_WHOLE_LINE_MIN_N=0)
+        const char* wv = std::getenv("RR_WHOLE_LINE_MIN_N");
+        e->whole_line_min_n = wv ? std::strtoll(wv, nullptr, 10) : kWholeLineMinN;
     }
-    DeviceGuard g(device);
     struct A {
         void** ptr;
         size_t bytes;
@@ -1788,6 +1811,13 @@ int rr_seed(rr_env* e, uint64_t seed, void* stream)
     if (cs != hipStreamCaptureStatusNone)
         return fail(RR_EINVAL, "rr_seed: the stream is being captured into a graph (seed before capturing: "
                                "replays read the key current when they run)");
+    // a launch of this handle queued on ANOTHER stream may still read the key: the new key must not
+    // land under it. Only then the device is synchronised; the usual single-stream
+    // caller keeps the stream-ordered write.
+    if (e->launched && e->last_stream != stream) {
+        err = hipDeviceSynchronize();
+        if (err != hipSuccess) return hip_fail(err, "rr_seed: synchronise the handle's earlier stream");
+    }
     seed_words(seed, e->kp.seed_w);
     err = hipMemcpyAsync(e->d_kp, &e->kp, sizeof(KParams), hipMemcpyHostToDevice, s);
     if (err == hipSuccess) err = hipStreamSynchronize(s);  // e->kp is pageable host memory: wait until it is read
@@ -1805,6 +1835,8 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
         hipLaunchKernelGGL(reset_kernel<3>, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->kp, b,
                            mask, obs, e->state64);
     hipError_t err = hipGetLastError();
+    e->last_stream = stream;
+    e->launched = true;
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_reset: launch");
 }
 
@@ -1840,7 +1872,7 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
         const uint32_t nn = (uint32_t)e->n;
         const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
         const uint32_t mode =
-            e->p.flags | (counter ? kModeCounter : 0u) | (e->n > kWholeLineMinN ? kModeWholeLines : 0u);
+            e->p.flags | (counter ? kModeCounter : 0u) | (e->n > e->whole_line_min_n ? kModeWholeLines : 0u);
         const bool soa = e->p.flags & RR_FLAG_ACTION_SOA;
         // small N (at most ~2 main waves per SIMD): helper waves draw the reset candidates
         const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;
@@ -1882,6 +1914,8 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return hip_fail(err, "rr_step: launch");
     e->steps++;
+    e->last_stream = stream;
+    e->launched = true;
     return RR_OK;
 }
 }  // namespace
@@ -2351,6 +2385,8 @@ int launch_rollout(rr_env* e, const char* who, bool multi, const float* params, 
     }
     if (err != hipSuccess) return hip_fail(err, (std::string(who) + ": launch").c_str());
     e->steps += io.T;
+    e->last_stream = stream;
+    e->launched = true;
     return RR_OK;
 }
 }  // namespace

@@ -150,3 +150,36 @@ def test_committed_traces_quote_the_upper_median_of_this_machine_code(tmp_path, 
     monkeypatch.setattr(bench, "_isa_hashes", lambda: {name: "other"})
     d, why = bench.stored_rocprof(6, 64, 20)
     assert d is None and "no file" in why
+
+
+def test_committed_traces_of_another_launch_mode_are_not_quoted(tmp_path, monkeypatch):
+    """the line's frac quotes only traces recorded with the running command's launch
+    mode (graph replays at K >= 8): of three graph traces and two direct ones of the same code, the
+    upper median of the graph ones; with no graph trace, none (the reason names the other mode).
+    PMC traffic takes the lower median (a larger byte count would raise a bandwidth: ADVICE r4)."""
+    import json
+
+    import bench
+
+    name = "void step_kernel<6, 0, false, true, 4, false>(...)"
+    for tag, mean, launch in (("a", 4800.0, "graph"), ("b", 4300.0, "direct: tools/libbench_timed.so"),
+                              ("c", 4500.0, "graph"), ("d", 4000.0, "direct: x"), ("e", 4900.0, "graph")):
+        d = tmp_path / "profiles" / "r9" / tag
+        d.mkdir(parents=True)
+        (d / "rocprof_step_k20_n64.json").write_text(json.dumps(
+            {"kernel": "step_kernel<6,RK4>", "kernel_name": name, "isa_hash": "h1", "mean_ns": mean,
+             "launch": launch}))
+        (d / "pmc_traffic_n64.json").write_text(json.dumps(
+            {"kernel": "step_kernel<6,RK4>", "kernel_name": name, "isa_hash": "h1", "traffic_bytes": mean * 1000}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "_isa_hashes", lambda: {name: "h1"})
+    d, src = bench.stored_rocprof(6, 64, 20, launch="graph")
+    assert d["mean_ns"] == 4800.0 and d["median_of"].startswith("3 files") and "graph launches only" in d["selection"]
+    d, src = bench.stored_rocprof(6, 64, 20, launch="direct")
+    assert d["mean_ns"] == 4300.0  # upper median of 4000 / 4300
+    d, why = bench.stored_rocprof(6, 64, 20, launch="eager")
+    assert d is None and "other launch mode" in why
+    traffic, src = bench.stored_traffic(6, 64)
+    assert traffic == 4500.0 * 1000  # lower median of five
+    assert bench.launch_kind("graph") == "graph" and bench.launch_kind("direct: tools/x") == "direct"
+    assert bench.launch_kind("rr_step per step") == "eager"

@@ -16,10 +16,21 @@ def _env6():
     return ENV_CONFIG_6DOF
 
 
-def _check_rows(model, g, out, label):
+def _state_err(model, a, b, norm, circ_theta=False):
+    """Per-component floored-relative state error. circ_theta (3DOF): theta compared on the circle,
+    so that a value within rounding of the 0 / 2pi wrap point (fp32 vs fp64 wrapping it to opposite
+    ends) is not a 2pi error."""
+    e = floored_rel(a, b, norm)
+    if model == 3 and circ_theta:
+        d = np.abs(np.asarray(a, np.float64)[:, 2] - np.asarray(b, np.float64)[:, 2])
+        e[:, 2] = np.minimum(d, 2 * np.pi - d) / np.maximum(np.abs(b[:, 2]), norm[2])
+    return e
+
+
+def _check_rows(model, g, out, label, tol_state=TOL_STATE, tol_reward=TOL_REWARD, circ_theta=False):
     ns = 14 if model == 6 else 7
     norm = g["normalizer"][:ns]
-    e_state = floored_rel(out["state_out"], g["state_out"], norm).max(1)
+    e_state = _state_err(model, out["state_out"], g["state_out"], norm, circ_theta).max(1)
     e_obs = floored_rel(out["obs"], g["obs"], 1.0).max(1)
     e_rew = floored_rel(out["reward"], g["reward"], 1.0)
     e_terms = floored_rel(out["terms"], g["terms"], 1.0).max(1)
@@ -30,11 +41,15 @@ def _check_rows(model, g, out, label):
         label, e_state.max(), e_obs.max(), e_rew.max(), e_terms.max(), (~done_eq).sum(), (~bv_eq).sum(),
         (~ev_eq).sum())
     print(msg)
-    e_comp = floored_rel(out["state_out"], g["state_out"], norm)
+    e_comp = _state_err(model, out["state_out"], g["state_out"], norm, circ_theta)
     worst = np.argmax(e_comp, axis=0)
     print("  per-component max:", " ".join("%d:%.2g(row %d g%d)" % (j, e_comp[worst[j], j], worst[j],
                                                                      g["group"][worst[j]]) for j in range(ns)))
-    bad = np.where((e_state > TOL_STATE) | (e_obs > TOL_STATE) | (e_rew > TOL_REWARD) | (e_terms > TOL_REWARD)
+    if model == 3 and circ_theta:  # obs[2] = theta / 2pi: the same circle, period 1
+        d = np.abs(out["obs"][:, 2].astype(np.float64) - g["obs"][:, 2])
+        e_obs = np.maximum(floored_rel(np.delete(out["obs"], 2, 1), np.delete(g["obs"], 2, 1), 1.0).max(1),
+                           np.minimum(d, 1.0 - d))
+    bad = np.where((e_state > tol_state) | (e_obs > tol_state) | (e_rew > tol_reward) | (e_terms > tol_reward)
                    | ~done_eq | ~bv_eq | ~ev_eq)[0]
     for i in bad[:10]:
         print("  row", i, "group", g["group"][i], "state_err", e_state[i], "rew", out["reward"][i], g["reward"][i],
@@ -118,6 +133,69 @@ def test_oracle_parity_6dof_65536(oracle_mod):
     g["group"] = rows["group"]
     g["normalizer"] = np.array(cfg.normalizer[:14])
     _check_rows(6, g, out, "6DOF oracle N=65536")
+
+
+def _random_states3(n, seed=0):
+    """Seeded 3DOF states [x, z, theta, vx, vz, omega, m] spanning the golden rows' envelope: 10 %
+    near the ground (z in [0.01, 5] m, descending: ground events), 10 % with theta within 0.03 rad
+    of the 0 / 2pi wrap point (omega up to 1 rad/s carries them across it), the bounds faces
+    (|x| up to 140 > x_bound 135)."""
+    rng = np.random.default_rng(seed)
+    s = np.zeros((n, 7))
+    s[:, 0] = rng.uniform(-140, 140, n)
+    s[:, 1] = np.where(rng.random(n) < 0.1, rng.uniform(0.01, 5, n), rng.uniform(5, 680, n))
+    w = rng.random(n)
+    s[:, 2] = np.where(w < 0.05, rng.uniform(0, 0.03, n),
+                       np.where(w < 0.1, rng.uniform(2 * np.pi - 0.03, 2 * np.pi, n),
+                                rng.uniform(np.pi / 2 - 1.2, np.pi / 2 + 1.2, n)))
+    s[:, 3] = rng.uniform(-40, 40, n)
+    s[:, 4] = rng.uniform(-100, 20, n)
+    s[:, 5] = rng.uniform(-1, 1, n)
+    s[:, 6] = rng.uniform(30e3, 51e3, n)
+    ic = np.tile(np.float32([100, 500, np.pi / 2, -10, -50, 0, 50e3]), (n, 1))
+    ic[:, 3] = rng.uniform(-11, -9, n).astype(np.float32)
+    ic[:, 4] = rng.uniform(-55, -45, n).astype(np.float32)
+    a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+    return ic, s.astype(np.float32).astype(np.float64), a
+
+
+def _oracle_rows(oracle_mod, model, n, seed, integrator="rk45"):
+    ic, s, a = _random_states6(n, seed) if model == 6 else _random_states3(n, seed)
+    rows = dict(group=np.zeros(n, np.int8), ic=ic, state_in=s, action=a)
+    kw = oracle_mod.ENV_CONFIG_6DOF if model == 6 else oracle_mod.DEFAULTS_3DOF
+    cfg = oracle_mod.make_cfg(model, integrator=integrator, **kw)
+    ref = oracle_mod.step(cfg, ic, 0.0, s, a, nthreads=8)
+    ref["event"] = ref["status"] == 1
+    g = dict(ref)
+    g["group"] = rows["group"]
+    g["normalizer"] = np.array(cfg.normalizer[:14 if model == 6 else 7])
+    return rows, g
+
+
+def test_oracle_parity_3dof_65536(oracle_mod):
+    """N = 65536 seeded 3DOF rows (ground events, theta across the 0 / 2pi wrap, bounds faces):
+    GPU RK4 step vs the CPU oracle (scipy RK45 + event) within the north star's 1e-5; done,
+    bounds and event flags identical on every row."""
+    n = 65536
+    rows, g = _oracle_rows(oracle_mod, 3, n, seed=11)
+    th0, th1 = rows["state_in"][:, 2], g["state_out"][:, 2]
+    wrapped = np.abs(th1 - th0) > np.pi
+    assert wrapped.sum() > 500 and g["event"].sum() > 1000 and g["bounds_violation"].sum() > 100
+    out = run_rows(3, rows)
+    _check_rows(3, g, out, "3DOF oracle N=65536", circ_theta=True)
+
+
+@pytest.mark.parametrize("model,n", [(3, 4096), (6, 4096), (3, 65536 + 17)])
+def test_euler_vs_oracle_euler(oracle_mod, model, n):
+    """BASELINE configs[1] ("3DOF N=4096 fp32, Euler"): the GPU's RR_INT_EULER step is explicit
+    Euler of the reference RHS (simulator.py:88-130 / :259-294) with the event root on Euler's
+    line (oracle/rocket_oracle.c euler_step) — within 1e-6 floored-relative of the fp64 oracle on
+    state, obs, reward and terms, flags identical, ground events and theta wraps included."""
+    rows, g = _oracle_rows(oracle_mod, model, n, seed=23 + model, integrator="euler")
+    assert g["event"].sum() > n // 40
+    out = run_rows(model, rows, integrator="euler", **(_env6() if model == 6 else {}))
+    _check_rows(model, g, out, "%dDOF Euler vs oracle Euler N=%d" % (model, n), tol_state=1e-6, tol_reward=1e-6,
+                circ_theta=True)
 
 
 def test_full_size_properties_6dof():

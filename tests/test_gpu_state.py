@@ -435,3 +435,83 @@ def test_seed_is_stream_ordered_and_refused_inside_a_capture():
         d.step(act)
     torch.cuda.synchronize()
     assert torch.equal(c.obs, d.obs) and torch.equal(c.get_state()[0], d.get_state()[0])
+
+
+@pytest.mark.parametrize("model,n,forced", [(6, 20003, True), (3, 20003, True), (6, (1 << 20) + 5, False)])
+def test_whole_line_done_path_is_bitwise_the_partial_line_path(model, n, forced, monkeypatch):
+    """above RR_WHOLE_LINE_MIN_N (default 1 << 20 envs) the plain step kernel stores the
+    terminal return / length and the reset v0 from EVERY lane of a wave that has a done lane, as
+    whole lines. That path (forced at 20 003 envs with RR_WHOLE_LINE_MIN_N=0, and at its default
+    threshold just past 1 M envs) against the partial-line path (threshold above N), both on the
+    plain kernel (RR_HELP_MAX_N=0), with auto-reset, Monitor returns and TimeLimit 7: obs, reward,
+    done / truncated, terms, state, v0, counter words, running returns and the done lists
+    (indices, terminal rows, returns, lengths) are bitwise equal at every step."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    monkeypatch.setenv("RR_HELP_MAX_N", "0")
+    kw = _env6() if model == 6 else {}
+    mk = lambda: RocketBatch(n, model=model, device="cuda:0", max_episode_steps=7, episode_stats=True,  # noqa: E731
+                             compute_terms=True, **kw)
+    if forced:
+        monkeypatch.setenv("RR_WHOLE_LINE_MIN_N", "0")
+    else:
+        monkeypatch.delenv("RR_WHOLE_LINE_MIN_N", raising=False)
+    a = mk()
+    monkeypatch.setenv("RR_WHOLE_LINE_MIN_N", str(1 << 40))
+    b = mk()
+    a.reset()
+    b.reset()
+    ends = 0
+    for t, act in enumerate(_actions(n, a.action_dim, 18, 13)):
+        oa = [x.clone() for x in a.step(act)]
+        ob = b.step(act)
+        for x, y in zip(oa, ob):
+            assert torch.equal(x, y), t
+        assert torch.equal(a.terms, b.terms), t
+        ia, toa, ra, la = a.fetch_done()
+        ib, tob, rb, lb = b.fetch_done()
+        np.testing.assert_array_equal(ia, ib)
+        np.testing.assert_array_equal(toa, tob)
+        np.testing.assert_array_equal(ra, rb)
+        np.testing.assert_array_equal(la, lb)
+        ends += len(ia)
+    assert ends >= 2 * n  # every env ended at least twice (TimeLimit 7 over 18 steps)
+    ca, cb = a.checkpoint(), b.checkpoint()
+    for k in ca:
+        assert torch.equal(ca[k], cb[k]), k
+
+
+def test_seed_on_another_stream_waits_for_the_handles_launches():
+    """steps of a handle queued on stream A, then rr_seed on stream B without any
+    synchronise of the caller: the seed waits for the device (the handle's last launch went to
+    another stream), so the queued steps read the OLD key — bitwise a twin that synchronised
+    before seeding — and every later step the new one."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 65536
+    mk = lambda: RocketBatch(n, model=6, device="cuda:0", max_episode_steps=2, **_env6())  # noqa: E731
+    a, b = mk(), mk()
+    for e in (a, b):
+        e.reset()
+    acts = _actions(n, 3, 12, 8)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    sa.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(sa):
+        for act in acts[:8]:  # TimeLimit 2: every env resets on every second step, keyed on the seed
+            a.step(act)
+    with torch.cuda.stream(sb):
+        a.seed(4321)
+    for act in acts[:8]:
+        b.step(act)
+    torch.cuda.synchronize()
+    b.seed(4321)
+    torch.cuda.current_stream().wait_stream(sa)
+    for act in acts[8:]:
+        a.step(act)
+        b.step(act)
+    torch.cuda.synchronize()
+    assert torch.equal(a.obs, b.obs)
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)

@@ -115,7 +115,12 @@ def _gpu_step(model, s, a, integrator="rk4", auto_reset=True, n_steps=1):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model", [6, 3])
-def test_fast_kernel_ends_non_finite_episodes(model):
+@pytest.mark.parametrize("help_max", [None, "0"])
+def test_fast_kernel_ends_non_finite_episodes(model, help_max, monkeypatch):
+    """Both step kernels: the helper-wave kernel (N <= RR_HELP_MAX_N, default) and the plain one
+    (RR_HELP_MAX_N=0, what every N > 131 072 runs)."""
+    if help_max is not None:
+        monkeypatch.setenv("RR_HELP_MAX_N", help_max)
     n = 300  # ragged: 4.7 waves
     s, a = _clean(model, n, seed=model)
     sb, ab, bad = _inject(model, s, a)
@@ -157,9 +162,15 @@ def test_fast_kernel_without_auto_reset_keeps_reporting_done(model):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model", [6, 3])
-def test_exact_mode_stops_like_the_oracle(model, oracle_mod):
+@pytest.mark.parametrize("lean", [False, True])
+def test_exact_mode_stops_like_the_oracle(model, lean, oracle_mod, monkeypatch):
     """DOPRI5 exact mode terminates on non-finite rows (status -1, done) with the oracle's
-    state; the other rows bitwise as in a clean batch."""
+    state; the other rows bitwise as in a clean batch. lean: the 6DOF lean two-waves-per-SIMD
+    kernel (RR_EXACT_LEAN_MIN_N=0; what N above CUs x 256 runs)."""
+    if lean:
+        if model == 3:
+            pytest.skip("the lean exact kernel is 6DOF only")
+        monkeypatch.setenv("RR_EXACT_LEAN_MIN_N", "0")
     n = 128
     s, a = _clean(model, n, seed=11)
     sb, ab, bad = _inject(model, s, a)
@@ -176,3 +187,66 @@ def test_exact_mode_stops_like_the_oracle(model, oracle_mod):
     assert fin.sum() >= 3  # the non-finite-action rows keep their (finite) input state
     np.testing.assert_allclose(out["state"][bad][fin], orc["state_out"][bad][fin].astype(np.float32), rtol=1e-6,
                                atol=1e-6)
+
+
+def _nan_equal(x, y):
+    import torch
+
+    return bool(((x == y) | (torch.isnan(x) & torch.isnan(y))).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", [6, 3])
+@pytest.mark.parametrize("per_step", [False, True])
+def test_rollout_kernels_end_non_finite_episodes(model, per_step):
+    """the on-device rollout (rr_rollout_collect, one launch, in its own translation
+    unit; per_step: rr_rollout_step) ends an episode whose state turns non-finite, as rr_step
+    does: rows with a NaN / inf state component step to status -1 (terms plane), done, and
+    restart from finite initial conditions (the next collect's obs are finite); every other env's
+    rollout buffers, outputs and state are bitwise those of a twin batch without the bad rows
+    (a NaN in one env's MFMA column reaches no other env)."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout, MlpActorCritic
+
+    n = 4096 + 37
+    ns, na = (14, 3) if model == 6 else (7, 2)
+    kw = ENV_CONFIG_6DOF if model == 6 else {}
+    torch.manual_seed(5)
+    pol = MlpActorCritic(ns, na).cuda()
+    bad = np.array([3, 64, 65, 700, 4100])
+    cols = np.array([0, 4, ns - 1, 6 if model == 6 else 2, 3])
+    vals = [float("nan"), float("inf"), float("nan"), -float("inf"), float("nan")]
+    ros = []
+    for poison in (False, True):
+        env = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=800, compute_terms=True, **kw)
+        ro = DeviceRollout(env, pol, n_steps=1, one_launch=True, per_step=per_step, seed=3)
+        st, v0, _ = env.get_state()
+        if poison:
+            for r, c, v in zip(bad, cols, vals):
+                st[c, r] = v
+        env.set_state(st, v0=v0)
+        ros.append(ro)
+    good = torch.ones(n, dtype=torch.bool, device="cuda:0")
+    good[torch.as_tensor(bad, device="cuda:0")] = False
+    for k in range(2):
+        for ro in ros:
+            ro.collect()
+        torch.cuda.synchronize()
+        clean, dirty = ros
+        status = dirty.env.terms[-1]
+        if k == 0:
+            assert (status[~good] == -1.0).all() and (dirty.env.done[~good] == 1).all(), status[~good]
+        assert torch.isfinite(dirty.env.obs[~good]).all()  # auto-reset to finite initial conditions
+        for name in ("obs", "actions", "values", "log_probs", "starts", "rewards", "advantages", "returns",
+                     "last_value", "last_done"):
+            x, y = getattr(clean, name), getattr(dirty, name)
+            assert _nan_equal(x[..., good] if x.dim() == 1 else x[:, good], y[..., good] if y.dim() == 1 else
+                              y[:, good]), (name, k)
+        for name in ("obs", "reward", "done", "truncated"):
+            assert torch.equal(getattr(clean.env, name)[good], getattr(dirty.env, name)[good]), name
+        assert torch.equal(clean.env.terms[:, good], dirty.env.terms[:, good])
+        assert torch.equal(clean.env.get_state()[0][:, good], dirty.env.get_state()[0][:, good])
+    for ro in ros:
+        ro.env.close()

@@ -71,3 +71,55 @@ def test_oracle_rhs_matches_reference_formulas(oracle_mod):
     assert dy[3] == pytest.approx(500e3 / 40e3 - 9.81)
     assert np.all(dy[[4, 5, 10, 11, 12]] == 0)
     assert dy[13] == pytest.approx(-500e3 / (9.81 * 360))
+
+
+@pytest.mark.parametrize("model", [6, 3])
+def test_euler_oracle_is_one_rhs_evaluation(oracle_mod, model, golden6, golden3):
+    """RO_INT_EULER (the restatement behind the GPU's RR_INT_EULER, BASELINE configs[1]): on the
+    golden inputs, rows without a ground event are y0 + dt f(y0) with f the oracle's reference RHS
+    (one evaluation, nfev 1), then renormalised / wrapped; rows with an event end on Euler's line
+    with the altitude at 0; status 1 exactly where the altitude changes sign over the step."""
+    g = golden6 if model == 6 else golden3
+    kw = oracle_mod.ENV_CONFIG_6DOF if model == 6 else oracle_mod.DEFAULTS_3DOF
+    cfg = oracle_mod.make_cfg(model, integrator="euler", **kw)
+    o = oracle_mod.step(cfg, g["ic"], g["t_in"], g["state_in"], g["action"])
+    ev = 0 if model == 6 else 1
+    assert (o["nfev"] == 1).all()
+    mg, mt = cfg.max_gimbal, cfg.max_thrust
+    checked = events = 0
+    for i in range(0, len(g["group"]), 7):
+        a = g["action"][i].astype(np.float64)
+        u = np.float32([a[0] * mg, a[1] * mg, (a[2] + 1) / 2.0 * mt]) if model == 6 else \
+            np.float32([a[0] * mg, (a[1] + 1) / 2.0 * mt])
+        y0 = g["state_in"][i]
+        f0 = oracle_mod.rhs(cfg, y0, u)
+        y1 = y0 + cfg.dt * f0
+        crosses = (y0[ev] <= 0 <= y1[ev]) or (y0[ev] >= 0 >= y1[ev])
+        assert o["status"][i] == (1 if crosses else 0), i
+        if crosses and y1[ev] != 0:
+            s = y0[ev] / (y0[ev] - y1[ev])
+            y1 = y0 + (s * cfg.dt) * f0
+            assert abs(y1[ev]) < 1e-9
+            events += 1
+        if model == 6:
+            y1[6:10] /= np.linalg.norm(y1[6:10])
+        else:
+            y1[2] = np.fmod(np.fmod(y1[2], 2 * np.pi) + 2 * np.pi, 2 * np.pi)
+        np.testing.assert_allclose(o["state_out"][i], y1, rtol=1e-13, atol=1e-11)
+        checked += 1
+    assert checked > 250 and events > 10
+
+
+@pytest.mark.parametrize("model", [6, 3])
+def test_euler_oracle_converges_to_the_reference_step(oracle_mod, model, golden6, golden3):
+    """Consistency of the Euler restatement with the reference's RK45 step: over a step of
+    dt = 1e-4 the two agree to O(dt^2) (floored-relative < 1e-6 on rows without an event)."""
+    g = golden6 if model == 6 else golden3
+    kw = dict(oracle_mod.ENV_CONFIG_6DOF if model == 6 else oracle_mod.DEFAULTS_3DOF, timestep=1e-4)
+    eu = oracle_mod.step(oracle_mod.make_cfg(model, integrator="euler", **kw), g["ic"], g["t_in"], g["state_in"],
+                         g["action"])
+    rk = oracle_mod.step(oracle_mod.make_cfg(model, **kw), g["ic"], g["t_in"], g["state_in"], g["action"])
+    ok = (eu["status"] == 0) & (rk["status"] == 0)
+    assert ok.sum() > 0.8 * len(ok)
+    e = oracle_mod.floored_rel(eu["state_out"][ok], rk["state_out"][ok], g["normalizer"])
+    assert e.max() < 1e-6, e.max()
