@@ -107,6 +107,8 @@ constexpr int32_t kMaxEpisodeSteps = 0xFFFF;
 // past the MALL" (N > kWholeLineMinN: the done path's 4-B scalars leave as whole lines)
 constexpr uint32_t kModeCounter = 0x80000000u;
 constexpr uint32_t kModeWholeLines = 0x40000000u;
+// (RR_AB_VEC_MODE) the caller's obs pointer is 16-B aligned: the obs tile leaves as float4 stores
+constexpr uint32_t kModeObsVec = 0x20000000u;
 // ~200 B of state, action and outputs per env and step: above ~1M envs a step's working set
 // passes the 256 MB MALL and partial lines become DRAM read-modify-writes (at 524 288, inside
 // it, the whole-line stores measured 2-4 % slower; at 4 194 304 10 % faster). RR_WHOLE_LINE_MIN_N
@@ -139,6 +141,9 @@ struct KParams {
     // after `flags` they shifted the fields above and the kernel's kernarg scalar loads regrouped
     // (+2 % per step at N = 65536, A/B r02l)
     uint32_t el_mask, ep_shift;
+#if defined(RR_AB_REWARD2)
+    float att_cs[3], land_cs[3];  // signed squares c |c| of att_c / land_c (axes 0 and 2)
+#endif
 };
 
 // The parameters read after the integration (reward, bounds, obs). Copied out of the
@@ -152,6 +157,9 @@ struct HotParams {
     float half_thrust, alfa, beta, eta, gamma, delta, kappa, xi;
     float waypoint, land_r2, land_v2;
     float att_c[3], land_c[3];
+#if defined(RR_AB_REWARD2)
+    float att_cs[3], land_cs[3];
+#endif
     float omega_lt, zero_h;
     uint32_t att_never, land_always, flags;
 };
@@ -177,6 +185,12 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
         H.bhi[j] = P.bhi[j];
         H.att_c[j] = P.att_c[j];
         H.land_c[j] = P.land_c[j];
+#if defined(RR_AB_REWARD2)
+        H.att_cs[j] = P.att_cs[j];
+        H.land_cs[j] = P.land_cs[j];
+        asm volatile("" : "+v"(H.att_cs[j]));
+        asm volatile("" : "+v"(H.land_cs[j]));
+#endif
         asm volatile("" : "+v"(H.blo[j]));
         asm volatile("" : "+v"(H.bhi[j]));
         asm volatile("" : "+v"(H.att_c[j]));
@@ -850,11 +864,29 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         const float rh1 = above ? s[1] : 0.0f, rh2 = above ? s[2] : 0.0f;
         const float vh0 = s[3] + (above ? 2.0f : 1.0f);
         const float tau_inv = above ? 1.0f / 20.0f : 1.0f / 100.0f;
+#if defined(RR_DIAG_REWARD_NOTRANS)  // diagnostic build only (tools/step_ab.py): no transcendental in the chain
+        float nrh = rh0 * rh0 + rh1 * rh1 + rh2 * rh2;
+        float t_go = nrh * (vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
+        const float xx = t_go * tau_inv;
+        float f = (-v0 * fminf(1e3f, nrh)) * (xx * (1.0f - xx * (0.5f - xx * (1.0f / 6.0f))));
+        float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
+        t[0] = P.alfa * (e0 * e0 + e1 * e1 + e2 * e2);
+#elif defined(RR_AB_REWARD2)
+        // 1 / max(1e-3, |r^|) = min(1e3, rsq(|r^|^2)) beside |r^| = sqrt(.): two independent
+        // transcendentals instead of sqrt -> max -> rcp in sequence (rsq(0) = inf -> 1e3)
+        const float rr = rh0 * rh0 + rh1 * rh1 + rh2 * rh2;
+        float nrh = fsqrt(rr);
+        float t_go = nrh * frsq(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
+        float f = (-v0 * fminf(1e3f, frsq(rr))) * one_minus_exp_neg(t_go * tau_inv);
+        float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
+        t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1 + e2 * e2);
+#else
         float nrh = fsqrt(rh0 * rh0 + rh1 * rh1 + rh2 * rh2);
         float t_go = nrh * frsq(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
         float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * one_minus_exp_neg(t_go * tau_inv);
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
         t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1 + e2 * e2);
+#endif
         // thrust_penalty = beta * T (denormalised, float32)
         t[1] = P.beta * ((a[2] + 1.0f) * P.half_thrust);
         t[2] = P.eta;
@@ -866,10 +898,27 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         float R02 = 2.0f * (x * z + y * w);
         float mR12 = 2.0f * (x * w - y * z);
         float R22 = w * w - x * x - y * y + z * z;
+#if defined(RR_DIAG_REWARD_NOTRANS)
+        float ra = R00 * R00 + mR01 * mR01;
+        float rc = R22 * R22 + mR12 * mR12;
+#elif defined(RR_AB_REWARD2)
+        // X < r c  <=>  X |X| < r^2 c |c| (the signed square is strictly increasing): no sqrt
+        const float ra2 = R00 * R00 + mR01 * mR01, rc2 = R22 * R22 + mR12 * mR12;
+        const float xa = R00 * fabsf(R00), xc = R22 * fabsf(R22);
+        float sb_ = fabsf(R02);
+        const bool att = (!(P.att_never & 1u) & (xa < ra2 * P.att_cs[0])) | (!(P.att_never & 2u) & (sb_ > P.att_c[1])) |
+                         (!(P.att_never & 4u) & (xc < rc2 * P.att_cs[2]));
+        const bool att_ok = (P.land_always != 0u) | (xa > ra2 * P.land_cs[0]) | (sb_ < P.land_c[1]) |
+                            (xc > rc2 * P.land_cs[2]);
+#else
         float ra = fsqrt(R00 * R00 + mR01 * mR01);
         float rc = fsqrt(R22 * R22 + mR12 * mR12);
+#endif
         // q was renormalised after the step (|q|^2 = 1 to fp32 rounding), so sin b = R02
         // without the division by |q|^2 (R00, R22 and the cos b radii are homogeneous)
+#if defined(RR_AB_REWARD2)
+        t[3] = att ? P.gamma : 0.0f;
+#else
         float sb = fabsf(R02);
         const bool att = (!(P.att_never & 1u) & (R00 < ra * P.att_c[0])) | (!(P.att_never & 2u) & (sb > P.att_c[1])) |
                          (!(P.att_never & 4u) & (R22 < rc * P.att_c[2]));
@@ -877,6 +926,7 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         // _check_landing (rocket_env.py:1040-1061); any() over angles and omega is the reference's
         const bool att_ok = (P.land_always != 0u) | (R00 > ra * P.land_c[0]) | (sb < P.land_c[1]) |
                             (R22 > rc * P.land_c[2]);
+#endif
         const bool om_ok = (fabsf(s[10]) < P.omega_lt) | (fabsf(s[11]) < P.omega_lt) | (fabsf(s[12]) < P.omega_lt);
         float r2 = s[0] * s[0] + s[1] * s[1] + s[2] * s[2];
         float v2 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
@@ -989,7 +1039,9 @@ __device__ __forceinline__ bool physics_step(const KParams& P, const float* a, c
     integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
     const float g0 = y0[EV], g1 = y1[EV];
     const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
+#if !defined(RR_DIAG_NO_EVENT)  // diagnostic build only: the ground-event root skipped
     if (event) event_step<MODEL, INTEG>(P, c, y0, f0, y1);
+#endif
     post_integrate<MODEL>(y1);
     return event;
 }
@@ -1123,7 +1175,11 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
             const uint32_t base = (blockIdx.x * WPB + k) * kWave;
             const uint32_t ih = min(base + lane, n - 1);
             const uint32_t cwh = (base < n && (mode & kModeCounter)) ? at(B.counter, ih) : 0u;
+#if defined(RR_DIAG_IDLE_HELPERS)  // diagnostic build only: the helper waves draw nothing
+            if (false) {
+#else
             if ((mode & RR_FLAG_AUTO_RESET) && base < n) {
+#endif
                 float s_[NS], v_;
                 ResetStream key = reset_stream(P.seed_w, P.id_off + base + lane, cwh);
                 sample_ic<MODEL>(P, key, s_, v_);
@@ -1182,7 +1238,11 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     }
 
     const bool event = physics_step<MODEL, INTEG>(P, a, y0, y1);
+#if defined(RR_DIAG_NO_NONFINITE)  // diagnostic build only
+    const bool nf = false;
+#else
     const bool nf = nonfinite<NS>(y1);
+#endif
     bool bv;
     float t[NT];
     const float r = reward_terms<MODEL>(H, y1, a, v0, bv, t);
@@ -1195,7 +1255,11 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     // Done compaction: one ballot per wave; lane 0 stores the wave's 64-bit done mask
     // (every wave writes its word each step, so no clearing and no atomics; the host
     // side expands the masks into the sorted index list, rr_fetch_done).
+#if defined(RR_DIAG_NO_DONE_TAIL)  // diagnostic build only: done lanes take no terminal-row / reset path
+    const bool dv = false;
+#else
     const bool dv = done && valid;
+#endif
     const uint64_t m = __ballot(dv);
     if (lane == 0) B.done_bits[wave_idx] = m;
     if (m) {
@@ -1251,8 +1315,30 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
         store_obs_tile<OW, kWave>(lds[wv], ow, make_rsrc(io.obs, (uint64_t)OW * plane), wave_base, lane, nvalid,
                                   io.obs_vec_ok);
     } else {
+    #if defined(RR_AB_OBS_DIRECT)  // A/B: obs rows stored from registers as 16-B pieces (no LDS tile)
+        if (valid) {
+            const rsrc_t orr = make_rsrc(io.obs, (uint64_t)NS * plane);
+            const uint32_t ro = NS == 14 ? (i << 6) - (i << 3) : i * (NS * 4u);
+#pragma unroll
+            for (int j = 0; j + 4 <= NS; j += 4)
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(o[j]), __float_as_uint(o[j + 1]),
+                                                             __float_as_uint(o[j + 2]), __float_as_uint(o[j + 3])},
+                                                       orr, (int)(ro + j * 4), 0, kOutAux);
+            if constexpr (NS % 4 == 2)
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, orr,
+                                                      (int)(ro + (NS - 2) * 4), 0, kOutAux);
+            else if constexpr (NS % 4 == 3)
+                __builtin_amdgcn_raw_buffer_store_b96(
+                    u32x3{__float_as_uint(o[NS - 3]), __float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, orr,
+                    (int)(ro + (NS - 3) * 4), 0, kOutAux);
+        }
+#elif defined(RR_AB_VEC_MODE)
+        store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
+                                  (mode & kModeObsVec) != 0u);
+#else
         store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
                                   io.obs_vec_ok);
+#endif
     }
 }
 
@@ -1364,8 +1450,14 @@ extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model,
     // lean (6DOF above one wave per SIMD, the caller's choice): 256 registers, two waves per SIMD
     // hide each other's fp64 latency (147.6 vs 176.6 us at N = 524 288); otherwise the in-loop
     // dense output (no event re-derivation, no spills: 28.9 vs 32.1 us at 65 536), profiles/r04/ab_lean/
+#if defined(RR_AB_EXACT_HALF)
+    if (model == RR_MODEL_6DOF && lean)  // 32 envs per wave: twice the workgroups
+        hipLaunchKernelGGL((step_exact_kernel<6, true>), dim3((unsigned)((b.n + kBlock / 2 - 1) / (kBlock / 2))),
+                           dim3(kBlock), 0, s, x, b, o, state64);
+#else
     if (model == RR_MODEL_6DOF && lean)
         hipLaunchKernelGGL((step_exact_kernel<6, true>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);
+#endif
     else if (model == RR_MODEL_6DOF)
         hipLaunchKernelGGL((step_exact_kernel<6, false>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);
     else
@@ -1535,6 +1627,10 @@ KParams make_kparams(const rr_params& p)
             if (M > pi) k.land_always |= 1u << ax;
             else k.land_c[ax] = (float)std::cos(M);
         }
+#if defined(RR_AB_REWARD2)
+        k.att_cs[ax] = k.att_c[ax] * std::fabs(k.att_c[ax]);
+        k.land_cs[ax] = k.land_c[ax] * std::fabs(k.land_c[ax]);
+#endif
     }
     k.omega_lt = ceil_f(p.omega_lim[0]);
     k.zero_h = floor_f(1e-3);
@@ -1857,6 +1953,11 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     io.terms = terms;
     io.obs_vec_ok = ((uintptr_t)obs & 15u) == 0;
     const Bufs b = bufs_of(e);
+#if defined(RR_AB_VEC_MODE)
+    const uint32_t vec_mode = io.obs_vec_ok ? kModeObsVec : 0u;
+#else
+    const uint32_t vec_mode = 0u;
+#endif
     hipStream_t s = (hipStream_t)stream;
     const bool m6 = e->p.model == RR_MODEL_6DOF;
     const bool euler = e->p.integrator == RR_INT_EULER;
@@ -1872,7 +1973,7 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
         const uint32_t nn = (uint32_t)e->n;
         const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
         const uint32_t mode =
-            e->p.flags | (counter ? kModeCounter : 0u) | (e->n > e->whole_line_min_n ? kModeWholeLines : 0u);
+            e->p.flags | (counter ? kModeCounter : 0u) | (e->n > e->whole_line_min_n ? kModeWholeLines : 0u) | vec_mode;
         const bool soa = e->p.flags & RR_FLAG_ACTION_SOA;
         // small N (at most ~2 main waves per SIMD): helper waves draw the reset candidates
         const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;
