@@ -1035,9 +1035,10 @@ def main():
         traffic, traffic_src = None, "PMC traffic files cover the headline configuration (RK4, no Monitor, no gather)"
         rp, rp_src = None, "rocprofv3 files cover the headline configuration"
     if args.integrator == "euler":
-        parity = ("NON-PARITY speed mode (BASELINE configs[1] 'Euler integrator'): explicit Euler misses the "
-                  "reference's RK45 by 30-130x the 1e-5 bar (SURVEY.md §7; tests/test_gpu_envs.py::"
-                  "test_euler_mode_is_declared_non_parity)")
+        parity = ("explicit Euler of the reference RHS (BASELINE configs[1] 'Euler integrator'): within 1e-6 of the "
+                  "oracle's fp64 Euler restatement (oracle/rocket_oracle.c euler_step; tests/test_gpu_parity.py::"
+                  "test_euler_vs_oracle_euler); a declared NON-PARITY mode against the reference's RK45 step (30-130x "
+                  "its 1e-5 bar, tests/test_gpu_envs.py::test_euler_mode_is_declared_non_parity)")
     elif args.integrator == "dopri5":
         parity = ("exact mode: fp64 scipy RK45 + brentq restated, <= 4.4e-9 floored-relative vs the reference's "
                   "rows (tests/test_gpu_exact.py)")

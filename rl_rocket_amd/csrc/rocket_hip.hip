@@ -1164,8 +1164,10 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t n = n_envs;
     if constexpr (HELP) {
+#if !defined(RR_DIAG_NO_BARRIER)  // diagnostic build only: no flag clear, no workgroup barrier
         if (wv < (uint32_t)WPB && lane == 0) cflag[wv] = 0u;
         __syncthreads();  // flags cleared before any helper can publish
+#endif
         if (wv >= (uint32_t)WPB) {
             // the helper role reads its parameters through the device copy (B.kp): kernel-argument
             // values it used were loaded in the kernel's entry block and kept live into the main

@@ -99,6 +99,19 @@ class MlpActorCritic(nn.Module):
 POLICY_PRECISIONS = {"fp32": 0, "bf16": 1, "fp16x3": 2}  # RR_POLICY_FP32 / RR_POLICY_BF16 / RR_POLICY_FP16X3
 
 
+# folded fp32 tanh of the rollout pack (rocket_policy.inc kPolFoldTanh): c = 2 log2 e
+FOLD_C = 2.88539008177792681
+
+
+def _rowsum(w):
+    """Row sums of a [rows][cols] weight in fp64, column by column (the pack kernel's order)."""
+    w = w.double()
+    acc = torch.zeros(w.shape[0], dtype=torch.float64, device=w.device)
+    for q in range(w.shape[1]):
+        acc = acc + w[:, q]
+    return acc
+
+
 class PolicyPack:
     """Packs an ``MlpActorCritic``'s weights into the fragment-ordered buffer of the fused
     HIP policy kernel (layout: rl_rocket_amd/csrc/rocket_policy.inc, offsets from
@@ -188,6 +201,13 @@ class PolicyPack:
                 return torch.cat([hi.view(torch.float32), lo.view(torch.float32)])
 
             l1, l2, bscale = split(l1), split(l2), 65536.0
+        if self.prec == 0:  # the folded fp32 tanh (rocket_policy.inc kPolFoldTanh), fp64 then one rounding
+            c = FOLD_C
+            self.buf[base + o["L1A"]: base + o["L1A"] + l1.numel()] = (c * l1.double()).float()
+            self.buf[base + o["B1"]: base + o["B1"] + 64] = (c * b1.double()).float()[self.b_i]
+            self.buf[base + o["L2A"]: base + o["L2A"] + l2.numel()] = (-2.0 * c * l2.double()).float()
+            self.buf[base + o["B2"]: base + o["B2"] + 64] = (c * (b2.double() + _rowsum(w2))).float()[self.b_i]
+            return
         self.buf[base + o["L1A"]: base + o["L1A"] + l1.numel()] = l1
         self.buf[base + o["B1"]: base + o["B1"] + 64] = b1[self.b_i] * bscale
         self.buf[base + o["L2A"]: base + o["L2A"] + l2.numel()] = l2
@@ -223,10 +243,17 @@ class PolicyPack:
         p, o, na = self.policy, self.off, self.act_dim
         self._tower(p.pi_net, o["PI"])
         self._tower(p.vf_net, o["VF"])
-        self.buf[o["HA"]: o["HA"] + 64 * na] = p.action_net.weight[:, self.b_i].reshape(-1)
-        self.buf[o["HV"]: o["HV"] + 64] = p.value_net.weight[0, self.b_i]
-        self.buf[o["HB"]: o["HB"] + na] = p.action_net.bias
-        self.buf[o["VB"]: o["VB"] + 1] = p.value_net.bias
+        wa, wv = p.action_net.weight, p.value_net.weight
+        if self.prec == 0:  # folded: the heads read r2 with tanh = 1 - 2 r2
+            self.buf[o["HA"]: o["HA"] + 64 * na] = (-2.0 * wa[:, self.b_i]).reshape(-1)
+            self.buf[o["HV"]: o["HV"] + 64] = -2.0 * wv[0, self.b_i]
+            self.buf[o["HB"]: o["HB"] + na] = (p.action_net.bias.double() + _rowsum(wa)).float()
+            self.buf[o["VB"]: o["VB"] + 1] = (p.value_net.bias.double() + _rowsum(wv)).float()
+        else:
+            self.buf[o["HA"]: o["HA"] + 64 * na] = wa[:, self.b_i].reshape(-1)
+            self.buf[o["HV"]: o["HV"] + 64] = wv[0, self.b_i]
+            self.buf[o["HB"]: o["HB"] + na] = p.action_net.bias
+            self.buf[o["VB"]: o["VB"] + 1] = p.value_net.bias
         self.buf[o["LS"]: o["LS"] + na] = p.log_std
         return self.buf
 

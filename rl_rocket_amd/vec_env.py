@@ -464,13 +464,18 @@ class RocketVecEnv(_VecEnvBase):
 
 
 class RocketVectorEnv(RocketVecEnv):
-    """The same batched env with the ``gym.vector.VectorEnv`` (gym 0.21) surface the north
-    star names: ``observation_space`` / ``action_space`` are the BATCHED Boxes
-    (num_envs, dim) and ``single_observation_space`` / ``single_action_space`` the per-env
-    ones; ``reset() -> obs``, ``step(actions) -> (obs, rewards, dones, infos)`` with auto-reset
-    and ``infos[i]["terminal_observation"]`` for done envs (SyncVectorEnv semantics);
-    ``reset_async`` / ``reset_wait`` / ``step_async`` / ``step_wait`` / ``close`` / ``seed``.
-    Stepping is the same fused kernel as ``RocketVecEnv``."""
+    """The same batched env with the ``gym.vector.VectorEnv`` surface of gym 0.21.0 — the
+    version the reference pins (requirements.txt:29) — that the north star names:
+    ``observation_space`` / ``action_space`` are the BATCHED Boxes (num_envs, dim) and
+    ``single_observation_space`` / ``single_action_space`` the per-env ones; ``reset() -> obs``
+    (no seed / options keywords, no info), ``step(actions) -> (obs, rewards, dones, infos)`` with
+    ``infos`` a LIST of per-env dicts, as gym 0.21's ``SyncVectorEnv.step_wait`` returns, auto-reset
+    of done envs and, as there, ``infos[i]["terminal_observation"]`` holding the last obs of a done
+    env; ``reset_async`` / ``reset_wait`` / ``step_async`` / ``step_wait`` / ``close`` / ``seed``.
+    It does NOT follow the later gym (>= 0.24) / gymnasium vector contract (5-tuple steps,
+    dict-of-arrays infos, ``final_observation``). Stepping is the same fused kernel as
+    ``RocketVecEnv``, whose SB3 ``VecEnv`` contract shares the list-of-dicts infos and the
+    ``terminal_observation`` key."""
 
     def __init__(self, num_envs, model="6DOF", **kwargs):
         super().__init__(num_envs, model=model, **kwargs)

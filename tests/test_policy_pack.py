@@ -23,37 +23,50 @@ def test_pack_reference_matches_layout(ns, na):
     buf = pk.pack_reference().numpy()
     o = pk.off
     kp1 = (ns + 1) // 2
-    g = lambda t: t.detach().numpy()  # noqa: E731
+    g = lambda t: t.detach().numpy().astype(np.float64)  # noqa: E731
+    # the folded fp32 tanh (rocket_policy.inc kPolFoldTanh; tanh(x) = 1 - 2 / (1 + 2^(c x))): c = 2 log2 e
+    # on layer 1, -2c on W2 and c (b2 + row sums of W2) on b2, -2 on the head weights and + row sums on
+    # their biases; fp64, one rounding to fp32
+    c = 2.0 * np.log2(np.e)
+    f32 = np.float32
+
+    def rowsum(w):  # column by column, as the pack kernel
+        acc = np.zeros(w.shape[0])
+        for q in range(w.shape[1]):
+            acc = acc + w[:, q]
+        return acc
+
     for tw, net in ((o["PI"], pol.pi_net), (o["VF"], pol.vf_net)):
         w1, b1, w2, b2 = g(net[0].weight), g(net[0].bias), g(net[2].weight), g(net[2].bias)
+        b2f = b2 + rowsum(w2)
         for m in range(2):
             for s in range(kp1):
                 for lane in range(64):
                     k = 2 * s + (lane >> 5)
-                    ref = w1[32 * m + (lane & 31), k] if k < ns else 0.0
+                    ref = f32(c * w1[32 * m + (lane & 31), k]) if k < ns else 0.0
                     assert buf[tw + o["L1A"] + (m * kp1 + s) * 64 + lane] == ref
             for half in range(2):
                 for reg in range(16):
-                    assert buf[tw + o["B1"] + (m * 2 + half) * 16 + reg] == b1[32 * m + _row(reg, half)]
-                    assert buf[tw + o["B2"] + (m * 2 + half) * 16 + reg] == b2[32 * m + _row(reg, half)]
+                    assert buf[tw + o["B1"] + (m * 2 + half) * 16 + reg] == f32(c * b1[32 * m + _row(reg, half)])
+                    assert buf[tw + o["B2"] + (m * 2 + half) * 16 + reg] == f32(c * b2f[32 * m + _row(reg, half)])
             for t in range(2):
                 for gg in range(4):
                     for lane in range(64):
                         for r in range(4):
-                            ref = w2[32 * m + (lane & 31), 32 * t + _row(4 * gg + r, lane >> 5)]
+                            ref = f32(-2.0 * c * w2[32 * m + (lane & 31), 32 * t + _row(4 * gg + r, lane >> 5)])
                             assert buf[tw + o["L2A"] + (((m * 2 + t) * 4 + gg) * 64 + lane) * 4 + r] == ref
     wa, wv = g(pol.action_net.weight), g(pol.value_net.weight)
     for a in range(na):
         for m in range(2):
             for half in range(2):
                 for reg in range(16):
-                    assert buf[o["HA"] + a * 64 + (m * 2 + half) * 16 + reg] == wa[a, 32 * m + _row(reg, half)]
+                    assert buf[o["HA"] + a * 64 + (m * 2 + half) * 16 + reg] == -2.0 * wa[a, 32 * m + _row(reg, half)]
     for m in range(2):
         for half in range(2):
             for reg in range(16):
-                assert buf[o["HV"] + (m * 2 + half) * 16 + reg] == wv[0, 32 * m + _row(reg, half)]
-    assert np.array_equal(buf[o["HB"]:o["HB"] + na], g(pol.action_net.bias))
-    assert buf[o["VB"]] == g(pol.value_net.bias)[0]
+                assert buf[o["HV"] + (m * 2 + half) * 16 + reg] == -2.0 * wv[0, 32 * m + _row(reg, half)]
+    assert np.array_equal(buf[o["HB"]:o["HB"] + na], (g(pol.action_net.bias) + rowsum(wa)).astype(f32))
+    assert buf[o["VB"]] == f32(g(pol.value_net.bias)[0] + rowsum(wv)[0])
     assert np.array_equal(buf[o["LS"]:o["LS"] + na], g(pol.log_std))
     assert pk.size == o["LS"] + 4
 

@@ -26,7 +26,9 @@ def main():
     dev = torch.device("cuda", 0)
     out = torch.zeros((256 * 512,), device=dev)
     res = {"what": "2 waves per SIMD (256 workgroups x 8 waves); role 0 MFMA only, 1 VALU only, 2 one of each per "
-                   "SIMD; m rounds of 4 fp32 32x32x2 MFMAs, v rounds of 4 v_fma_f32", "runs": []}
+                   "SIMD; m rounds of 4 fp32 32x32x2 MFMAs, v rounds of 4 v_fma_f32; role 3 v rounds of 4 v_exp_f32, "
+                   "4 one MFMA wave + one exp wave per SIMD, 5 one stream with 2 v_exp_f32 after each MFMA",
+           "runs": []}
 
     def timed(role, m, v):
         def go():
@@ -55,6 +57,16 @@ def main():
     for m, v in ((32, 512), (64, 1024), (128, 2048), (64, 0), (0, 1024)):
         row = {"m": m, "v": v}
         for role in (0, 1, 2):
+            row["role%d_us" % role] = timed(role, m, v)
+        res["runs"].append(row)
+        print(json.dumps(row), flush=True)
+    # transcendentals (v_exp_f32) beside / between fp32 MFMAs: role 3 exp alone, 4 one MFMA wave and
+    # one exp wave per SIMD, 5 both in one stream (2 exps after each MFMA); role 0 / 3 at the same m / v
+    # are the references (role 5 issues 8 exps per round of 4 MFMAs: v = 2 m rounds of 4 exps)
+    for m in (32, 64, 128):
+        v = 2 * m
+        row = {"m": m, "v_exp": v}
+        for role in (0, 3, 4, 5):
             row["role%d_us" % role] = timed(role, m, v)
         res["runs"].append(row)
         print(json.dumps(row), flush=True)
