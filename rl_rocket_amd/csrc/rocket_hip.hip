@@ -1211,12 +1211,36 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
 
     // ---- all loads first (one memory round trip per wave); the counter word first, so the
     // reset candidate below is drawn while the state planes are still in flight ----
+#if defined(RR_AB_LOAD_ORDER)
+    // A/B: loads in the order the step consumes them (HELP kernels: the counter word last, it is
+    // used after the integration only): action, then the 6DOF attitude / rates / mass that the
+    // RK4 stages read first, then v and r (the quadratures at the end), v0
+    uint32_t cw = 0u;
+    if (!HELP && use_counter) cw = bld_u(st_r, vo, cw_off);
+    float y0[NS], y1[NS], a[NA];
+    load_action<NA, ASOA>(make_rsrc(action, (uint64_t)NA * plane), vo, plane, a);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (MODEL == 6) {
+#pragma unroll
+        for (int j = 6; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) y0[j] = bld_f(st_r, vo, j * plane);
+    } else {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    float v0 = bld_f(st_r, vo, v0_off);
+    if (HELP && use_counter) cw = bld_u(st_r, vo, cw_off);
+#else
     uint32_t cw = use_counter ? bld_u(st_r, vo, cw_off) : 0u;
     float y0[NS], y1[NS], a[NA];
     load_action<NA, ASOA>(make_rsrc(action, (uint64_t)NA * plane), vo, plane, a);
 #pragma unroll
     for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
     float v0 = bld_f(st_r, vo, v0_off);
+#endif
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
     const CounterLayout CL(P);
