@@ -1463,7 +1463,7 @@ __global__ __launch_bounds__(kBlock) void copy_done_rows_kernel(const uint64_t* 
 
 // the exact TU's only entry point (hidden: not part of the C-ABI). bufs / io / xp point to the
 // Bufs / StepIO / XParams of the calling TU (same definitions, same layout).
-extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model, int lean, const void* xp,
+extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model, int variant, const void* xp,
                                                                         const void* bufs, const void* io,
                                                                         double* state64, unsigned grid, void* stream)
 {
@@ -1473,21 +1473,24 @@ extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model,
     std::memcpy(&o, io, sizeof(StepIO));
     const XParams* x = static_cast<const XParams*>(xp);
     hipStream_t s = (hipStream_t)stream;
-    // lean (6DOF above one wave per SIMD, the caller's choice): 256 registers, two waves per SIMD
-    // hide each other's fp64 latency (147.6 vs 176.6 us at N = 524 288); otherwise the in-loop
-    // dense output (no event re-derivation, no spills: 28.9 vs 32.1 us at 65 536), profiles/r04/ab_lean/
-#if defined(RR_AB_EXACT_HALF)
-    if (model == RR_MODEL_6DOF && lean)  // 32 envs per wave: twice the workgroups
-        hipLaunchKernelGGL((step_exact_kernel<6, true>), dim3((unsigned)((b.n + kBlock / 2 - 1) / (kBlock / 2))),
-                           dim3(kBlock), 0, s, x, b, o, state64);
-#else
-    if (model == RR_MODEL_6DOF && lean)
-        hipLaunchKernelGGL((step_exact_kernel<6, true>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);
-#endif
-    else if (model == RR_MODEL_6DOF)
-        hipLaunchKernelGGL((step_exact_kernel<6, false>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);
-    else
-        hipLaunchKernelGGL((step_exact_kernel<3, false>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);
+    // variant bit 0 = lean (6DOF above one wave per SIMD, the caller's choice): 256 registers, two
+    // waves per SIMD hide each other's fp64 latency (147.6 vs 176.6 us at N = 524 288); otherwise the
+    // in-loop dense output (no event re-derivation, no spills: 28.9 vs 32.1 us at 65 536,
+    // profiles/r04/ab_lean/). Bit 1 = [NA][N] action planes (RR_FLAG_ACTION_SOA).
+    const bool lean = variant & 1, soa = variant & 2;
+#define RR_LAUNCH_X(M, L, A) \
+    hipLaunchKernelGGL((step_exact_kernel<M, L, A>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64)
+    if (model == RR_MODEL_6DOF && lean) {
+        if (soa) RR_LAUNCH_X(6, true, true);
+        else RR_LAUNCH_X(6, true, false);
+    } else if (model == RR_MODEL_6DOF) {
+        if (soa) RR_LAUNCH_X(6, false, true);
+        else RR_LAUNCH_X(6, false, false);
+    } else {
+        if (soa) RR_LAUNCH_X(3, false, true);
+        else RR_LAUNCH_X(3, false, false);
+    }
+#undef RR_LAUNCH_X
     return (int)hipGetLastError();
 }
 #elif defined(RR_TU_COLLECT)
@@ -1991,9 +1994,9 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     if (e->p.integrator == RR_INT_DOPRI5) {
         // the exact kernels live in the second translation unit (rocket_exact.hip: compiled with a
         // register-pressure-first scheduler, no scratch spills)
-        const hipError_t xe = (hipError_t)rrx_launch_exact(m6 ? RR_MODEL_6DOF : RR_MODEL_3DOF,
-                                                           m6 && e->n > e->exact_lean_min_n, e->d_xp, &b, &io,
-                                                           e->state64, grid.x, s);
+        const int variant = (m6 && e->n > e->exact_lean_min_n ? 1 : 0) | ((e->p.flags & RR_FLAG_ACTION_SOA) ? 2 : 0);
+        const hipError_t xe = (hipError_t)rrx_launch_exact(m6 ? RR_MODEL_6DOF : RR_MODEL_3DOF, variant, e->d_xp, &b,
+                                                           &io, e->state64, grid.x, s);
         if (xe != hipSuccess) return hip_fail(xe, "rr_step: exact launch");
     } else {
         const uint32_t nn = (uint32_t)e->n;

@@ -22,8 +22,8 @@ def hashes():
 def test_every_translation_unit_hashed(hashes):
     names = list(hashes)
     assert any("step_kernel<6, 0, false, true, 4, false>" in k for k in names)  # main
-    assert any("step_exact_kernel<6, true>" in k for k in names)  # exact
-    assert any("step_exact_kernel<6, false>" in k for k in names)
+    assert any("step_exact_kernel<6, true, false>" in k for k in names)  # exact
+    assert any("step_exact_kernel<6, false, false>" in k for k in names)
     assert any("rollout_step_kernel<6, 0, 0, false" in k for k in names)  # main
     assert any("rollout_step_kernel<6, 0, 0, true" in k for k in names)  # collect
     assert all(len(v) == 16 for v in hashes.values())
