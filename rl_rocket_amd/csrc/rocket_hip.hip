@@ -1325,8 +1325,10 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     cw = CL.with_elapsed(cw, el);
 
     if (valid) {
+#if !defined(RR_DIAG_NO_STATE_STORE)  // diagnostic build only: the 14 state planes are not stored
 #pragma unroll
         for (int j = 0; j < NS; ++j) bst_f<SA>(st_r, y1[j], vo, j * plane);
+#endif
         if (use_counter) bst_u<SA>(st_r, cw, vo, (NS + 1) * plane);
         if (mode & RR_FLAG_EPISODE_STATS) bst_f<SA>(st_r, ret, vo, (NS + 2) * plane);
         store_outputs<NT, !ROWS>(io, i, vo, plane, n, r, done, trunc, t, bv, event ? 1.0f : (nf ? -1.0f : 0.0f));
@@ -1361,6 +1363,8 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
 #elif defined(RR_AB_VEC_MODE)
         store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
                                   (mode & kModeObsVec) != 0u);
+#elif defined(RR_DIAG_NO_OBS_STORE)  // diagnostic build only: no obs tile / stores
+        (void)nvalid;
 #else
         store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
                                   io.obs_vec_ok);
