@@ -812,8 +812,8 @@ __device__ __forceinline__ bool nonfinite(const float* y)
 
 // Sample one initial condition: gym Box.sample (uniform in [low, high], float32),
 // then q <- q/|q| (rocket_env.py:672-673); v0 = |IC velocity| (rocket_env.py:989-991).
-template <int MODEL>
-__device__ __forceinline__ void sample_ic(const KParams& P, ResetStream& k, float* s, float& v0)
+template <int MODEL, class IP>  // IP: KParams, or anything with its ic_low / ic_span (rol::ResetParams)
+__device__ __forceinline__ void sample_ic(const IP& P, ResetStream& k, float* s, float& v0)
 {
     constexpr int NS = Dims<MODEL>::NS;
 #pragma unroll
