@@ -515,3 +515,35 @@ def test_seed_on_another_stream_waits_for_the_handles_launches():
     assert torch.equal(a.obs, b.obs)
     for x, y in zip(a.get_state(), b.get_state()):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("integrator", ["rk4", "dopri5"])
+@pytest.mark.parametrize("model", [6, 3])
+def test_unaligned_obs_output_is_bitwise_the_aligned_one(model, integrator):
+    """The obs rows go out through each wave's LDS tile as 16-B stores when the obs pointer is
+    16-B aligned, else dword by dword (store_obs_tile; since round 5 also in the exact kernel).
+    A twin env writing its obs 4 bytes off alignment, with a ragged last wave, must produce the
+    same obs / reward / done bitwise at every step (auto-reset within the 40 steps)."""
+    import torch
+
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 4096 + 37
+    kw = _env6() if model == 6 else {}
+    mk = lambda: RocketBatch(n, model=model, device="cuda:0", max_episode_steps=15, integrator=integrator,  # noqa: E731
+                             **kw)
+    a, b = mk(), mk()
+    a.reset()
+    b.reset()
+    ns = a.state_dim
+    raw = torch.empty((n * ns + 1,), dtype=torch.float32, device="cuda:0")
+    obs_u = raw[1:].view(n, ns)
+    assert obs_u.data_ptr() % 16 != 0
+    out = (obs_u, torch.empty_like(b.reward), torch.empty_like(b.done), torch.empty_like(b.truncated))
+    for act in _actions(n, a.action_dim, 40, 7):
+        oa, ra, da, _ = a.step(act)
+        ob, rb, db, _ = b.step(act, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db)
+    a.close()
+    b.close()
