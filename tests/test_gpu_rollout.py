@@ -187,23 +187,23 @@ def test_policy_bootstrap_and_gae(prec):
     close(out2, ref, "fused bootstrap")
     assert torch.equal(st, done.float())
     close(val, vref, "value")
-    # GAE kernel vs the PyTorch scan
-    T = 16
-    r, v, s = torch.randn((T, n), device="cuda:0"), torch.randn((T, n), device="cuda:0"), \
-        (torch.rand((T, n), device="cuda:0") < 0.05).float()
-    lv, ld = torch.randn((n,), device="cuda:0"), (torch.rand((n,), device="cuda:0") < 0.05).float()
-    adv, ret = torch.empty_like(r), torch.empty_like(r)
-    _lib.check(lib.rr_gae(T, n, _ptr(r), _ptr(v), _ptr(s), _ptr(lv), _ptr(ld), 0.99, 0.95, _ptr(adv), _ptr(ret), None),
-               "rr_gae")
-    torch.cuda.synchronize()
-    last, ref_adv = torch.zeros(n, device="cuda:0"), torch.empty_like(r)
-    for t in reversed(range(T)):
-        nt = 1.0 - (ld if t == T - 1 else s[t + 1])
-        nv = lv if t == T - 1 else v[t + 1]
-        last = r[t] + 0.99 * nv * nt - v[t] + 0.99 * 0.95 * nt * last
-        ref_adv[t] = last
-    assert (adv - ref_adv).abs().max().item() < 1e-5
-    assert (ret - (ref_adv + v)).abs().max().item() < 1e-5
+    # GAE kernel vs the PyTorch scan (T = 37: the device scan runs in 16-step chunks, 16 + 16 + 5)
+    for T in (16, 37):
+        r, v, s = torch.randn((T, n), device="cuda:0"), torch.randn((T, n), device="cuda:0"), \
+            (torch.rand((T, n), device="cuda:0") < 0.05).float()
+        lv, ld = torch.randn((n,), device="cuda:0"), (torch.rand((n,), device="cuda:0") < 0.05).float()
+        adv, ret = torch.empty_like(r), torch.empty_like(r)
+        _lib.check(lib.rr_gae(T, n, _ptr(r), _ptr(v), _ptr(s), _ptr(lv), _ptr(ld), 0.99, 0.95, _ptr(adv), _ptr(ret),
+                              None), "rr_gae")
+        torch.cuda.synchronize()
+        last, ref_adv = torch.zeros(n, device="cuda:0"), torch.empty_like(r)
+        for t in reversed(range(T)):
+            nt = 1.0 - (ld if t == T - 1 else s[t + 1])
+            nv = lv if t == T - 1 else v[t + 1]
+            last = r[t] + 0.99 * nv * nt - v[t] + 0.99 * 0.95 * nt * last
+            ref_adv[t] = last
+        assert (adv - ref_adv).abs().max().item() < 1e-5, T
+        assert (ret - (ref_adv + v)).abs().max().item() < 1e-5, T
 
 
 @pytest.mark.parametrize("fused,prec", [(True, "fp32"), (False, "fp32"), (True, "bf16"), (True, "fp16x3")])
@@ -244,20 +244,21 @@ def test_fused_collect_matches_semantics(fused, prec):
     env.close()
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16x3"])
+@pytest.mark.parametrize("prec,T", [("fp32", 8), ("bf16", 8), ("fp16x3", 8), ("fp32", 37)])
 @pytest.mark.parametrize("model", [6, 3])
-def test_one_launch_rollout_bitwise_equals_two_launch(model, prec):
+def test_one_launch_rollout_bitwise_equals_two_launch(model, prec, T):
     """rr_rollout_collect (the whole rollout + GAE in one kernel) and rr_rollout_step (policy +
     env step in one kernel per step) against rr_policy_act + rr_step: every rollout buffer,
     the env outputs (incl. reward terms), the terminal rows and the env state bitwise equal
     over two collects (TimeLimit 6 < n_steps: truncation bootstraps and auto-resets inside the
-    rollout; ragged N: idle waves in the last workgroup)."""
+    rollout; ragged N: idle waves in the last workgroup; n_steps 37: the collect kernel's GAE
+    scan runs in 16-step chunks, 16 + 16 + 5)."""
     import torch
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
     from rl_rocket_amd.rollout import DeviceRollout
 
-    n, T = 4096 + 37, 8
+    n = 4096 + 37
     ns, na = (14, 3) if model == 6 else (7, 2)
     kw = ENV_CONFIG_6DOF if model == 6 else {}
     pol = _policy(ns, na, seed=3)
