@@ -1700,6 +1700,23 @@ XParams make_xparams(const rr_params& p)
     x.landing_radius = p.landing_radius;
     x.max_velocity = p.max_velocity;
     x.clamp_h0 = (p.flags & RR_FLAG_SCIPY_H0_CLAMP) ? 1 : 0;
+    {
+        const double pi = 3.14159265358979323846;
+        for (int ax = 0; ax < 3; ++ax) {  // as make_kparams' float thresholds, in fp64
+            const double L = p.att_limit[ax], M = p.land_att_limit[ax];
+            if (ax == 1) {
+                if (L >= pi / 2) x.att_never |= 1u << ax;
+                else x.att_c[ax] = std::sin(L);
+                if (M > pi / 2) x.land_always |= 1u << ax;
+                else x.land_c[ax] = std::sin(M);
+            } else {
+                if (L >= pi) x.att_never |= 1u << ax;
+                else x.att_c[ax] = std::cos(L);
+                if (M > pi) x.land_always |= 1u << ax;
+                else x.land_c[ax] = std::cos(M);
+            }
+        }
+    }
     return x;
 }
 
