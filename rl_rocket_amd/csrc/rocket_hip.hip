@@ -1163,6 +1163,11 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     // uniform, and every buffer store with a wave_base soffset became a waterfall loop
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t n = n_envs;
+#if defined(RR_DIAG_STAMPS)  // diagnostic build only (tools/step_stamps.py): phase clocks -> io.reward
+    const uint64_t dg_rt0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t dg_c0 = (uint32_t)__builtin_amdgcn_s_memtime();
+    uint32_t dg_c[4];
+#endif
     if constexpr (HELP) {
 #if !defined(RR_DIAG_NO_BARRIER)  // diagnostic build only: no flag clear, no workgroup barrier
         if (wv < (uint32_t)WPB && lane == 0) cflag[wv] = 0u;
@@ -1197,6 +1202,11 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     const uint32_t wave_idx = blockIdx.x * WPB + wv;
     const uint32_t wave_base = wave_idx * kWave;
     if (wave_base >= n) return;  // wave-uniform
+#if defined(RR_DIAG_STAMPS)
+    __builtin_amdgcn_sched_barrier(0);
+    dg_c[0] = (uint32_t)__builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     const uint32_t i = wave_base + lane;
     const bool valid = i < n;
     const uint32_t ic = valid ? i : n - 1;
@@ -1263,6 +1273,13 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
         sample_ic<MODEL>(P, key, ic_s, ic_v0);
     }
 
+#if defined(RR_DIAG_STAMPS)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) asm volatile("" ::"v"(y0[j]));
+    __builtin_amdgcn_sched_barrier(0);
+    dg_c[1] = (uint32_t)__builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     const bool event = physics_step<MODEL, INTEG>(P, a, y0, y1);
 #if defined(RR_DIAG_NO_NONFINITE)  // diagnostic build only
     const bool nf = false;
@@ -1277,6 +1294,11 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     ret += r;
     float o[NS];
     normalize_obs<NS>(y1, H.inv_norm, o);
+#if defined(RR_DIAG_STAMPS)
+    __builtin_amdgcn_sched_barrier(0);
+    dg_c[2] = (uint32_t)__builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 
     // Done compaction: one ballot per wave; lane 0 stores the wave's 64-bit done mask
     // (every wave writes its word each step, so no clearing and no atomics; the host
@@ -1370,6 +1392,20 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
                                   io.obs_vec_ok);
 #endif
     }
+#if defined(RR_DIAG_STAMPS)
+    // lanes 0..2: barrier / loads / compute cycles; 3: the tail (outputs issued); 4, 5: the wave's
+    // s_memrealtime start / end (100 MHz, low 32 bits, bit patterns in the float slots)
+    __builtin_amdgcn_sched_barrier(0);
+    dg_c[3] = (uint32_t)__builtin_amdgcn_s_memtime();
+    const uint32_t dg_rt1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    float dv_ = (float)(dg_c[0] - dg_c0);
+    dv_ = lane == 1 ? (float)(dg_c[1] - dg_c[0]) : dv_;
+    dv_ = lane == 2 ? (float)(dg_c[2] - dg_c[1]) : dv_;
+    dv_ = lane == 3 ? (float)(dg_c[3] - dg_c[2]) : dv_;
+    dv_ = lane == 4 ? __uint_as_float((uint32_t)dg_rt0) : dv_;
+    dv_ = lane == 5 ? __uint_as_float(dg_rt1) : dv_;
+    if (lane < 6 && valid) io.reward[i] = dv_;
+#endif
 }
 
 template <int MODEL>
