@@ -102,6 +102,30 @@ def test_exact_vs_oracle_65536(oracle_mod):
     _check(6, ref, out, np.array(cfg.normalizer[:14]), "DOPRI5 6DOF vs oracle N=65536")
 
 
+def test_exact_attitude_tests_at_the_limits(oracle_mod, lean):
+    """The exact kernel's attitude tests without inverse trig (cos / sin thresholds in fp64)
+    against the oracle's atan2 / asin on rows 1e-8 .. 1e-5 rad inside and outside the 1.5 rad limit
+    of both tested axes: the penalty term agrees row for row, both sides present."""
+    from test_gpu_parity import _near_limit_rows6, _zyx_of
+
+    n = 8192
+    ic, s, a, axis, d = _near_limit_rows6(n, 5, -8.0, -5.0)
+    rows = dict(ic=ic, state_in=s, action=a, t_in=np.zeros(n))
+    out = run_exact(6, rows, **_kw(6))
+    cfg = oracle_mod.make_cfg(6, **oracle_mod.ENV_CONFIG_6DOF)
+    ref = oracle_mod.step(cfg, ic, 0.0, s, a, nthreads=8)
+    # the reward reads the fp32 attitude: below ~1e-7 rad its rounding decides the side
+    e = _zyx_of(ref["state_out"][:, 6:10].astype(np.float32).astype(np.float64))
+    side = np.abs(e[np.arange(n), axis]) > 1.5
+    far = np.abs(d) > 1e-6
+    assert np.array_equal(side[far], d[far] > 0)
+    assert 0.3 < side.mean() < 0.7
+    att_ref = ref["terms"][:, 3] != 0
+    assert np.array_equal(att_ref, side)
+    att = out["terms"][:, 3] != 0
+    assert np.array_equal(att, att_ref), np.flatnonzero(att != att_ref)[:10]
+
+
 def test_exact_lean_kernel_is_bitwise_the_inloop_kernel(monkeypatch):
     """The lean kernel re-derives an event step's stages after the step loop: same inputs, same
     arithmetic, so every output is bitwise the in-loop kernel's, event rows included."""

@@ -120,6 +120,78 @@ def _random_states6(n, seed=0):
     return ic, s.astype(np.float32).astype(np.float64), a
 
 
+def _quat_from_zyx(a, b, c):
+    """q = (w, x, y, z) whose rotation gives the env's zyx angles a = atan2(-R01, R00),
+    b = asin(R02), c = atan2(-R12, R22) (rocket_env.py:852-855): q = qx(c) qy(b) qz(a)."""
+    def qa(axis, t):
+        q = np.zeros((len(t), 4))
+        q[:, 0] = np.cos(t / 2)
+        q[:, 1 + axis] = np.sin(t / 2)
+        return q
+
+    def mul(p, q):
+        w1, x1, y1, z1 = p.T
+        w2, x2, y2, z2 = q.T
+        return np.stack([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                         w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2], axis=1)
+    return mul(mul(qa(0, c), qa(1, b)), qa(2, a))
+
+
+def _zyx_of(q):
+    w, x, y, z = (q / np.linalg.norm(q, axis=1, keepdims=True)).T
+    a = np.arctan2(-2 * (x * y - z * w), w * w + x * x - y * y - z * z)
+    b = np.arcsin(np.clip(2 * (x * z + y * w), -1, 1))
+    c = np.arctan2(-2 * (y * z - x * w), w * w - x * x - y * y + z * z)
+    return np.stack([a, b, c], axis=1)
+
+
+def _near_limit_rows6(n, seed, lo, hi, limit=1.5):
+    """6DOF rows whose attitude sits just inside or just outside the attitude limit on axis 0
+    (atan2) or axis 1 (asin): angle = +-(limit + d), |d| = 10^U(lo, hi) of either sign; omega = 0 and
+    zero gimbal, so the step leaves the attitude as it is (up to renormalisation). Returns (ic,
+    state, action, axis, d)."""
+    rng = np.random.default_rng(seed)
+    axis = rng.integers(0, 2, n)
+    d = rng.choice([-1.0, 1.0], n) * 10.0 ** rng.uniform(lo, hi, n)
+    ang = rng.choice([-1.0, 1.0], n) * (limit + d)
+    a = np.where(axis == 0, ang, rng.uniform(-0.5, 0.5, n))
+    b = np.where(axis == 1, ang, rng.uniform(-0.5, 0.5, n))
+    c = rng.uniform(-3.0, 3.0, n)
+    s = np.zeros((n, 14))
+    s[:, 0] = rng.uniform(200, 500, n)
+    s[:, 1:3] = rng.uniform(-100, 100, (n, 2))
+    s[:, 3] = rng.uniform(-60, 0, n)
+    s[:, 4:6] = rng.uniform(-10, 10, (n, 2))
+    s[:, 6:10] = _quat_from_zyx(a, b, c)
+    s[:, 13] = rng.uniform(35e3, 45e3, n)
+    ic = np.tile(np.float32([500, 100, 100, -50, 0, 0, 1, 0, 0, 0, 0, 0, 0, 45e3]), (n, 1))
+    act = np.zeros((n, 3), np.float32)
+    act[:, 2] = rng.uniform(-1, 1, n).astype(np.float32)
+    return ic, s, act, axis, d
+
+
+def test_attitude_tests_at_the_limits_fast(oracle_mod):
+    """The fast kernel's attitude tests run without inverse trig (X < r cos L, |sin b| > sin L):
+    against the oracle's atan2 / asin on rows 1e-5 .. 1e-3 rad inside and outside the 1.5 rad
+    limit of both tested axes (beyond the fp32 attitude's rounding), the penalty term agrees row for
+    row and both sides of the limit are present."""
+    n = 8192
+    ic, s, a, axis, d = _near_limit_rows6(n, 3, -5.0, -3.0)
+    s = s.astype(np.float32).astype(np.float64)
+    rows = dict(group=np.zeros(n, np.int8), ic=ic, state_in=s, action=a)
+    out = run_rows(6, rows, **_env6())
+    cfg = oracle_mod.make_cfg(6, **oracle_mod.ENV_CONFIG_6DOF)
+    ref = oracle_mod.step(cfg, ic, 0.0, s, a, nthreads=8)
+    e = _zyx_of(ref["state_out"][:, 6:10].astype(np.float32).astype(np.float64))  # reward reads the fp32 attitude
+    side = np.abs(e[np.arange(n), axis]) > 1.5
+    assert np.array_equal(side, d > 0)  # the rows sit where they were put, after the step
+    assert 0.3 < side.mean() < 0.7
+    att_ref = ref["terms"][:, 3] != 0
+    att = out["terms"][:, 3] != 0
+    assert np.array_equal(att_ref, side)
+    assert np.array_equal(att, att_ref), np.flatnonzero(att != att_ref)[:10]
+
+
 def test_oracle_parity_6dof_65536(oracle_mod):
     """N = 65536 seeded rows: GPU step vs the CPU oracle (faithful scipy RK45 + event)."""
     n = 65536
