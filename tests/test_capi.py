@@ -48,6 +48,9 @@ def test_invalid_arguments_fail_cleanly_without_gpu():
     assert lib.rr_create(ctypes.byref(h), ctypes.byref(p), 16, 0, 0) == _lib.RR_EINVAL
     p.max_episode_steps = 800
     assert lib.rr_create(ctypes.byref(h), ctypes.byref(p), 0, 0, 0) == _lib.RR_EINVAL
+    # the largest batch: n * (state_dim + 3) * 4 B within 32-bit buffer offsets (tests/test_gpu_maxsize.py)
+    assert lib.rr_create(ctypes.byref(h), ctypes.byref(p), 0xFFFFFFFF // 68 + 1, 0, 0) == _lib.RR_EINVAL
+    assert b"32-bit" in lib.rr_last_error()
     for bad in (0x40, 0x40000000, 0x80000000):  # the high bits are the kernels' internal mode word
         p.flags = 0x1 | bad
         assert lib.rr_create(ctypes.byref(h), ctypes.byref(p), 16, 0, 0) == _lib.RR_EINVAL
