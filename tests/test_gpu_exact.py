@@ -126,6 +126,29 @@ def test_exact_attitude_tests_at_the_limits(oracle_mod, lean):
     assert np.array_equal(att, att_ref), np.flatnonzero(att != att_ref)[:10]
 
 
+def test_exact_landing_attitude_test_at_the_limits(oracle_mod, lean):
+    """The exact kernel's landing attitude test without inverse trig, rows 1e-8 .. 1e-5 rad either
+    side of a landing limit on each axis (test_gpu_parity._near_limit_landing_rows6): the landing
+    bonus agrees with the oracle's row for row, both sides present."""
+    import copy
+
+    from test_gpu_parity import LAND_LIMIT, _env6_land, _near_limit_landing_rows6, _zyx_of
+
+    n = 8192
+    ic, s, a, axis, d = _near_limit_landing_rows6(n, 6, -8.0, -5.0)
+    out = run_exact(6, dict(ic=ic, state_in=s, action=a, t_in=np.zeros(n)), **_env6_land())
+    kw = copy.deepcopy(oracle_mod.ENV_CONFIG_6DOF)
+    kw["landing_params"]["landing_attitude_limit"] = list(LAND_LIMIT)
+    ref = oracle_mod.step(oracle_mod.make_cfg(6, **kw), ic, 0.0, s, a, nthreads=8)
+    assert (ref["status"] == 1).all() and out["event"].all()
+    e = _zyx_of(ref["state_out"][:, 6:10].astype(np.float32).astype(np.float64))
+    inside = np.abs(e[np.arange(n), axis]) < np.array(LAND_LIMIT)[axis]
+    far = np.abs(d) > 1e-6
+    assert np.array_equal(inside[far], d[far] < 0) and 0.3 < inside.mean() < 0.7
+    assert np.array_equal(ref["terms"][:, 4] != 0, inside)
+    assert np.array_equal(out["terms"][:, 4] != 0, inside), np.flatnonzero((out["terms"][:, 4] != 0) != inside)[:10]
+
+
 def test_exact_lean_kernel_is_bitwise_the_inloop_kernel(monkeypatch):
     """The lean kernel re-derives an event step's stages after the step loop: same inputs, same
     arithmetic, so every output is bitwise the in-loop kernel's, event rows included."""
