@@ -129,7 +129,10 @@ const char* rr_last_error(void);
 
 /* Allocate N envs on `device`. env_id_offset = global id of env 0 (multi-GPU shards
  * use rank*N so every env has its own RNG stream). Envs start un-initialised: call
- * rr_reset before the first rr_step. */
+ * rr_reset before the first rr_step. 1 <= N and N * (state_dim + 3) * 4 <= 2^32 - 1 (the
+ * kernels address each plane / row block with 32-bit buffer offsets): at most 63 161 283
+ * 6DOF or 107 374 182 3DOF envs per handle, else RR_EINVAL; larger batches are several
+ * handles (shards). */
 int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset, int device);
 int rr_destroy(rr_env* e);
 int64_t rr_num_envs(const rr_env* e);
