@@ -102,6 +102,20 @@ def test_exact_vs_oracle_65536(oracle_mod):
     _check(6, ref, out, np.array(cfg.normalizer[:14]), "DOPRI5 6DOF vs oracle N=65536")
 
 
+def test_exact_vs_oracle_3dof_65536(oracle_mod):
+    """3DOF exact mode at N = 65 536 seeded rows (ground events, theta across the 0 / 2pi wrap,
+    bounds faces: test_gpu_parity._random_states3) vs the oracle, at the exact mode's bar."""
+    from test_gpu_parity import _random_states3
+
+    n = 65536
+    ic, s, a = _random_states3(n, seed=13)
+    out = run_exact(3, dict(ic=ic, state_in=s, action=a, t_in=np.zeros(n)))
+    cfg = oracle_mod.make_cfg(3, **oracle_mod.DEFAULTS_3DOF)
+    ref = oracle_mod.step(cfg, ic, 0.0, s, a, nthreads=8)
+    assert (ref["status"] == 1).sum() > 1000 and ref["bounds_violation"].sum() > 100
+    _check(3, ref, out, np.array(cfg.normalizer[:7]), "DOPRI5 3DOF vs oracle N=65536")
+
+
 def test_exact_attitude_tests_at_the_limits(oracle_mod, lean):
     """The exact kernel's attitude tests without inverse trig (cos / sin thresholds in fp64)
     against the oracle's atan2 / asin on rows 1e-8 .. 1e-5 rad inside and outside the 1.5 rad limit
