@@ -188,10 +188,20 @@ class TimedLoop:
                          ev[0], ev[1])
 
 
+def per_rank_rows(dist, dt, kern_ms, K):
+    """Every rank's own wall time and events figure of the timed region (at world > 1
+    the line shows each rank, so a straggling rank is visible, not only the max over ranks)."""
+    row = {"rank": dist.get_rank(), "wall_ms_per_step": dt / K * 1e3, "kernel_us": kern_ms * 1e3,
+           "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
+    rows = [None] * dist.get_world_size()
+    dist.all_gather_object(rows, row)
+    return rows
+
+
 def timed_region(args, env, pool, dev, dist, backend, launch, gather=None):
     """W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier + synchronize on
-    both sides; returns wall seconds (max over ranks) and the per-launch device time by HIP
-    events on the launch stream."""
+    both sides; returns wall seconds (max over ranks), the per-launch device time by HIP
+    events on the launch stream and, at world > 1, every rank's own pair of them."""
     import torch
 
     stream = torch.cuda.current_stream(dev)
@@ -225,12 +235,14 @@ def timed_region(args, env, pool, dev, dist, backend, launch, gather=None):
         if dist is not None:
             dist.barrier()
         per = sorted(a.elapsed_time(b) for a, b in evs)
+        ranks = None
         if dist is not None:
+            ranks = per_rank_rows(dist, dt, sum(per) / K, K)
             t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         return {"dt": dt, "kern_ms": sum(per) / K, "use_graph": False, "use_loop": False, "gs": 0,
-                "isolated_median_ms": per[K // 2], "isolated_min_ms": per[0]}
+                "isolated_median_ms": per[K // 2], "isolated_min_ms": per[0], "per_rank": ranks}
     loop = TimedLoop(env) if use_loop else None
     if use_loop:
         ev0.record(stream)
@@ -300,11 +312,14 @@ def timed_region(args, env, pool, dev, dist, backend, launch, gather=None):
     # device time per launch over the timed region (kernel + inter-kernel gap: an upper bound
     # on the kernel's own duration, so `achieved` is conservative)
     kern_ms = ev0.elapsed_time(ev1) / K
-    if dist is not None:  # max over ranks of the timed region
+    ranks = None
+    if dist is not None:  # every rank's own figures, then the max over ranks of the timed region
+        ranks = per_rank_rows(dist, dt, kern_ms, K)
         t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    return {"dt": dt, "kern_ms": kern_ms, "use_graph": use_graph, "use_loop": use_loop, "gs": gs}
+    return {"dt": dt, "kern_ms": kern_ms, "use_graph": use_graph, "use_loop": use_loop, "gs": gs,
+            "per_rank": ranks}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -941,7 +956,7 @@ def gather_leg_result(args, env, pool, dev, dist, backend, launch, n, world, K):
     greg = timed_region(args, env, pool, dev, dist, backend, "graph" if launch in ("loop", "isolated") else launch, g)
     return {
         "value": n * world * K / greg["dt"], "unit": "env-steps/s", "ms_per_step": greg["dt"] / K * 1e3,
-        "device_us_per_step": greg["kern_ms"] * 1e3,
+        "device_us_per_step": greg["kern_ms"] * 1e3, "per_rank": greg.get("per_rank"),
         "world_size": dist.get_world_size(), "backend": dist.get_backend(),
         "bytes_per_rank_per_step": g.n_pad * (env.state_dim + 2) * 4,
         "launch": "graph" if greg["use_graph"] else "eager (gloo stages through the host)",
@@ -1128,6 +1143,10 @@ def main():
                      "bytes_per_env_step": bytes_env},
     }
 
+    if reg.get("per_rank"):
+        walls = [r["wall_ms_per_step"] for r in reg["per_rank"]]
+        result["per_rank"] = reg["per_rank"]
+        result["per_rank_wall_max_over_min"] = max(walls) / min(walls)
     if args.integrator == "dopri5" and world == 1:
         # the exact mode is fp64 VALU work, not HBM-bound: its issue rate against the fp64 vector
         # peak from the committed counters of the same N and machine code (tools/exact_counters.py)

@@ -149,8 +149,13 @@ int rr_action_dim(const rr_env* e);
  * in the order of `stream` (launches queued on it before the call read the old key) and the
  * call returns once it has landed (it synchronises `stream`, nothing else); it applies to every
  * launch that runs after it, including replays of hipGraphs captured before it, at every N.
- * If the handle's last step / reset / rollout launch went to a DIFFERENT stream, the call first
- * synchronises the device, so that no launch still queued there reads a half-written key.
+ * Launches of the handle (step / reset / rollout) queued on OTHER streams since the last rr_seed
+ * are waited for on the device: the key copy waits on a per-handle event recorded on each of
+ * those streams (up to 8 distinct streams; past that, or when one of them no longer exists, the
+ * call synchronises the device), so no launch still queued there reads a half-written key, and
+ * nothing else on the device is waited for. NOT tracked: replays of hipGraphs (they are not
+ * launches of the handle) — the caller orders a replay queued on another stream before the seed
+ * (seed on the replay's stream, or synchronise it first).
  * RR_EINVAL while `stream` is being captured into a graph. */
 int rr_seed(rr_env* e, uint64_t seed, void* stream);
 /* Sample a fresh initial condition for every env where mask[i] != 0 (all when mask is
@@ -253,8 +258,16 @@ int rr_copy_terminal(rr_env* e, float* term_obs, float* term_return, int32_t* te
  * an on-device rollout: the MlpPolicy actor-critic (separate pi / vf towers, net_arch
  * [64, 64], tanh, state-independent log_std) runs as one fp32 MFMA launch per step.
  * Supported (obs_dim, act_dim): (14, 3) 6DOF, (7, 2) 3DOF.
- * precision: RR_POLICY_FP32 (default; v_mfma_f32_32x32x2_f32, exact fp32 products, the
- * SB3 policy's numbers to fp32 rounding) or RR_POLICY_BF16 (opt-in; v_mfma_f32_32x32x16_bf16
+ * precision: RR_POLICY_FP32 (default; v_mfma_f32_32x32x2_f32, exact fp32 products. The pack
+ * holds the tanh FOLDED into the weights: tanh(x) = 1 - 2 r, r = 1 / (1 + 2^(2 x log2 e)), with
+ * W1' = c W1, b1' = c b1, W2' = -2c W2, b2' = c (b2 + row sums of W2), heads W' = -2 W and
+ * b' = b + row sums of W (c = 2 log2 e; each folded value computed in fp64 and rounded once to
+ * fp32), so a hidden unit is v_exp_f32 + add + v_rcp_f32. The SB3 policy's numbers to a few fp32
+ * ulps of each weight and hidden unit: values / means within ~1e-5 of the fp32 MlpPolicy
+ * (tests/test_gpu_rollout.py). The PPO learner (rr_ppo_grad) packs and runs the UNfolded tanh,
+ * so the rollout's log_prob / value and the learner's recomputation on the same parameters agree
+ * to rounding, not bit for bit: at epoch 0 the ratio is 1 and approx_kl 0 only to ~1e-6 / ~1e-12
+ * (tests/test_gpu_ppo.py::test_rollout_and_learner_forwards_agree)) or RR_POLICY_BF16 (opt-in; v_mfma_f32_32x32x16_bf16
  * with fp32 accumulation: obs, the tower weights and the first hidden layer rounded to
  * bf16, everything else fp32) or RR_POLICY_FP16X3 (v_mfma_f32_32x32x16_f16 on operands split
  * into two fp16 halves, three MFMAs per k step: ~2^-21 relative products, fp32-level

@@ -20,7 +20,8 @@ EXACT_FLAGS = ["-mllvm", "-amdgpu-schedule-metric-bias=100"]
 SRC_COLLECT = os.path.join(HERE, "csrc", "rocket_collect.hip")
 COLLECT_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc", "rocket_rollout.inc", "rocket_ppo.inc",
-                                                 "rocket_exact.hip", "rocket_collect.hip")]
+                                                 "rocket_exact.hip", "rocket_collect.hip",
+                                                 "rocket_stamps.h")]
 HEADER = os.path.join(ROOT, "include", "rocket_hip.h")
 OUT = os.path.join(HERE, "librocket_hip.so")
 # benchmark-only helper (not part of the product ABI): bench.py's event-timed direct-launch region

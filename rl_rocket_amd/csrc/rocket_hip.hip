@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "rocket_hip.h"
+#include "rocket_stamps.h"
 
 
 namespace {
@@ -107,8 +108,6 @@ constexpr int32_t kMaxEpisodeSteps = 0xFFFF;
 // past the MALL" (N > kWholeLineMinN: the done path's 4-B scalars leave as whole lines)
 constexpr uint32_t kModeCounter = 0x80000000u;
 constexpr uint32_t kModeWholeLines = 0x40000000u;
-// (RR_AB_VEC_MODE) the caller's obs pointer is 16-B aligned: the obs tile leaves as float4 stores
-constexpr uint32_t kModeObsVec = 0x20000000u;
 // ~200 B of state, action and outputs per env and step: above ~1M envs a step's working set
 // passes the 256 MB MALL and partial lines become DRAM read-modify-writes (at 524 288, inside
 // it, the whole-line stores measured 2-4 % slower; at 4 194 304 10 % faster). RR_WHOLE_LINE_MIN_N
@@ -141,9 +140,6 @@ struct KParams {
     // after `flags` they shifted the fields above and the kernel's kernarg scalar loads regrouped
     // (+2 % per step at N = 65536, A/B r02l)
     uint32_t el_mask, ep_shift;
-#if defined(RR_AB_REWARD2)
-    float att_cs[3], land_cs[3];  // signed squares c |c| of att_c / land_c (axes 0 and 2)
-#endif
 };
 
 // The parameters read after the integration (reward, bounds, obs). Copied out of the
@@ -157,9 +153,6 @@ struct HotParams {
     float half_thrust, alfa, beta, eta, gamma, delta, kappa, xi;
     float waypoint, land_r2, land_v2;
     float att_c[3], land_c[3];
-#if defined(RR_AB_REWARD2)
-    float att_cs[3], land_cs[3];
-#endif
     float omega_lt, zero_h;
     uint32_t att_never, land_always, flags;
 };
@@ -185,12 +178,6 @@ __device__ __forceinline__ HotParams load_hot(const KParams& P)
         H.bhi[j] = P.bhi[j];
         H.att_c[j] = P.att_c[j];
         H.land_c[j] = P.land_c[j];
-#if defined(RR_AB_REWARD2)
-        H.att_cs[j] = P.att_cs[j];
-        H.land_cs[j] = P.land_cs[j];
-        asm volatile("" : "+v"(H.att_cs[j]));
-        asm volatile("" : "+v"(H.land_cs[j]));
-#endif
         asm volatile("" : "+v"(H.blo[j]));
         asm volatile("" : "+v"(H.bhi[j]));
         asm volatile("" : "+v"(H.att_c[j]));
@@ -864,29 +851,11 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         const float rh1 = above ? s[1] : 0.0f, rh2 = above ? s[2] : 0.0f;
         const float vh0 = s[3] + (above ? 2.0f : 1.0f);
         const float tau_inv = above ? 1.0f / 20.0f : 1.0f / 100.0f;
-#if defined(RR_DIAG_REWARD_NOTRANS)  // diagnostic build only (tools/step_ab.py): no transcendental in the chain
-        float nrh = rh0 * rh0 + rh1 * rh1 + rh2 * rh2;
-        float t_go = nrh * (vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
-        const float xx = t_go * tau_inv;
-        float f = (-v0 * fminf(1e3f, nrh)) * (xx * (1.0f - xx * (0.5f - xx * (1.0f / 6.0f))));
-        float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
-        t[0] = P.alfa * (e0 * e0 + e1 * e1 + e2 * e2);
-#elif defined(RR_AB_REWARD2)
-        // 1 / max(1e-3, |r^|) = min(1e3, rsq(|r^|^2)) beside |r^| = sqrt(.): two independent
-        // transcendentals instead of sqrt -> max -> rcp in sequence (rsq(0) = inf -> 1e3)
-        const float rr = rh0 * rh0 + rh1 * rh1 + rh2 * rh2;
-        float nrh = fsqrt(rr);
-        float t_go = nrh * frsq(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
-        float f = (-v0 * fminf(1e3f, frsq(rr))) * one_minus_exp_neg(t_go * tau_inv);
-        float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
-        t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1 + e2 * e2);
-#else
         float nrh = fsqrt(rh0 * rh0 + rh1 * rh1 + rh2 * rh2);
         float t_go = nrh * frsq(vh0 * vh0 + s[4] * s[4] + s[5] * s[5]);
         float f = (-v0 * frcp(fmaxf(1e-3f, nrh))) * one_minus_exp_neg(t_go * tau_inv);
         float e0 = s[3] - f * rh0, e1 = s[4] - f * rh1, e2 = s[5] - f * rh2;
         t[0] = P.alfa * fsqrt(e0 * e0 + e1 * e1 + e2 * e2);
-#endif
         // thrust_penalty = beta * T (denormalised, float32)
         t[1] = P.beta * ((a[2] + 1.0f) * P.half_thrust);
         t[2] = P.eta;
@@ -898,27 +867,10 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         float R02 = 2.0f * (x * z + y * w);
         float mR12 = 2.0f * (x * w - y * z);
         float R22 = w * w - x * x - y * y + z * z;
-#if defined(RR_DIAG_REWARD_NOTRANS)
-        float ra = R00 * R00 + mR01 * mR01;
-        float rc = R22 * R22 + mR12 * mR12;
-#elif defined(RR_AB_REWARD2)
-        // X < r c  <=>  X |X| < r^2 c |c| (the signed square is strictly increasing): no sqrt
-        const float ra2 = R00 * R00 + mR01 * mR01, rc2 = R22 * R22 + mR12 * mR12;
-        const float xa = R00 * fabsf(R00), xc = R22 * fabsf(R22);
-        float sb_ = fabsf(R02);
-        const bool att = (!(P.att_never & 1u) & (xa < ra2 * P.att_cs[0])) | (!(P.att_never & 2u) & (sb_ > P.att_c[1])) |
-                         (!(P.att_never & 4u) & (xc < rc2 * P.att_cs[2]));
-        const bool att_ok = (P.land_always != 0u) | (xa > ra2 * P.land_cs[0]) | (sb_ < P.land_c[1]) |
-                            (xc > rc2 * P.land_cs[2]);
-#else
         float ra = fsqrt(R00 * R00 + mR01 * mR01);
         float rc = fsqrt(R22 * R22 + mR12 * mR12);
-#endif
         // q was renormalised after the step (|q|^2 = 1 to fp32 rounding), so sin b = R02
         // without the division by |q|^2 (R00, R22 and the cos b radii are homogeneous)
-#if defined(RR_AB_REWARD2)
-        t[3] = att ? P.gamma : 0.0f;
-#else
         float sb = fabsf(R02);
         const bool att = (!(P.att_never & 1u) & (R00 < ra * P.att_c[0])) | (!(P.att_never & 2u) & (sb > P.att_c[1])) |
                          (!(P.att_never & 4u) & (R22 < rc * P.att_c[2]));
@@ -926,7 +878,6 @@ __device__ __forceinline__ float reward_terms(const HotParams& P, const float* s
         // _check_landing (rocket_env.py:1040-1061); any() over angles and omega is the reference's
         const bool att_ok = (P.land_always != 0u) | (R00 > ra * P.land_c[0]) | (sb < P.land_c[1]) |
                             (R22 > rc * P.land_c[2]);
-#endif
         const bool om_ok = (fabsf(s[10]) < P.omega_lt) | (fabsf(s[11]) < P.omega_lt) | (fabsf(s[12]) < P.omega_lt);
         float r2 = s[0] * s[0] + s[1] * s[1] + s[2] * s[2];
         float v2 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
@@ -1039,9 +990,7 @@ __device__ __forceinline__ bool physics_step(const KParams& P, const float* a, c
     integrate<MODEL, INTEG>(P, c, y0, P.h, y1, f0);
     const float g0 = y0[EV], g1 = y1[EV];
     const bool event = (g0 <= 0.0f && g1 >= 0.0f) || (g0 >= 0.0f && g1 <= 0.0f);
-#if !defined(RR_DIAG_NO_EVENT)  // diagnostic build only: the ground-event root skipped
     if (event) event_step<MODEL, INTEG>(P, c, y0, f0, y1);
-#endif
     post_integrate<MODEL>(y1);
     return event;
 }
@@ -1163,16 +1112,10 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     // uniform, and every buffer store with a wave_base soffset became a waterfall loop
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t n = n_envs;
-#if defined(RR_DIAG_STAMPS)  // diagnostic build only (tools/step_stamps.py): phase clocks -> io.reward
-    const uint64_t dg_rt0 = __builtin_amdgcn_s_memrealtime();
-    const uint32_t dg_c0 = (uint32_t)__builtin_amdgcn_s_memtime();
-    uint32_t dg_c[4];
-#endif
+    RR_STAMPS_BEGIN(4);  // diagnostic builds only (rocket_stamps.h)
     if constexpr (HELP) {
-#if !defined(RR_DIAG_NO_BARRIER)  // diagnostic build only: no flag clear, no workgroup barrier
         if (wv < (uint32_t)WPB && lane == 0) cflag[wv] = 0u;
         __syncthreads();  // flags cleared before any helper can publish
-#endif
         if (wv >= (uint32_t)WPB) {
             // the helper role reads its parameters through the device copy (B.kp): kernel-argument
             // values it used were loaded in the kernel's entry block and kept live into the main
@@ -1182,11 +1125,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
             const uint32_t base = (blockIdx.x * WPB + k) * kWave;
             const uint32_t ih = min(base + lane, n - 1);
             const uint32_t cwh = (base < n && (mode & kModeCounter)) ? at(B.counter, ih) : 0u;
-#if defined(RR_DIAG_IDLE_HELPERS)  // diagnostic build only: the helper waves draw nothing
-            if (false) {
-#else
             if ((mode & RR_FLAG_AUTO_RESET) && base < n) {
-#endif
                 float s_[NS], v_;
                 ResetStream key = reset_stream(P.seed_w, P.id_off + base + lane, cwh);
                 sample_ic<MODEL>(P, key, s_, v_);
@@ -1202,11 +1141,7 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     const uint32_t wave_idx = blockIdx.x * WPB + wv;
     const uint32_t wave_base = wave_idx * kWave;
     if (wave_base >= n) return;  // wave-uniform
-#if defined(RR_DIAG_STAMPS)
-    __builtin_amdgcn_sched_barrier(0);
-    dg_c[0] = (uint32_t)__builtin_amdgcn_s_memtime();
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    RR_STAMP(0);
     const uint32_t i = wave_base + lane;
     const bool valid = i < n;
     const uint32_t ic = valid ? i : n - 1;
@@ -1221,36 +1156,12 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
 
     // ---- all loads first (one memory round trip per wave); the counter word first, so the
     // reset candidate below is drawn while the state planes are still in flight ----
-#if defined(RR_AB_LOAD_ORDER)
-    // A/B: loads in the order the step consumes them (HELP kernels: the counter word last, it is
-    // used after the integration only): action, then the 6DOF attitude / rates / mass that the
-    // RK4 stages read first, then v and r (the quadratures at the end), v0
-    uint32_t cw = 0u;
-    if (!HELP && use_counter) cw = bld_u(st_r, vo, cw_off);
-    float y0[NS], y1[NS], a[NA];
-    load_action<NA, ASOA>(make_rsrc(action, (uint64_t)NA * plane), vo, plane, a);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (MODEL == 6) {
-#pragma unroll
-        for (int j = 6; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) y0[j] = bld_f(st_r, vo, j * plane);
-    } else {
-#pragma unroll
-        for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    float v0 = bld_f(st_r, vo, v0_off);
-    if (HELP && use_counter) cw = bld_u(st_r, vo, cw_off);
-#else
     uint32_t cw = use_counter ? bld_u(st_r, vo, cw_off) : 0u;
     float y0[NS], y1[NS], a[NA];
     load_action<NA, ASOA>(make_rsrc(action, (uint64_t)NA * plane), vo, plane, a);
 #pragma unroll
     for (int j = 0; j < NS; ++j) y0[j] = bld_f(st_r, vo, j * plane);
     float v0 = bld_f(st_r, vo, v0_off);
-#endif
     float ret = (mode & RR_FLAG_EPISODE_STATS) ? bld_f(st_r, vo, ret_off) : 0.0f;
     const HotParams H = load_hot<NS>(P);  // scalar loads overlap the HBM latency above
     const CounterLayout CL(P);
@@ -1273,19 +1184,9 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
         sample_ic<MODEL>(P, key, ic_s, ic_v0);
     }
 
-#if defined(RR_DIAG_STAMPS)
-#pragma unroll
-    for (int j = 0; j < NS; ++j) asm volatile("" ::"v"(y0[j]));
-    __builtin_amdgcn_sched_barrier(0);
-    dg_c[1] = (uint32_t)__builtin_amdgcn_s_memtime();
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    RR_STAMP_AFTER(1, y0, NS);  // the state landed
     const bool event = physics_step<MODEL, INTEG>(P, a, y0, y1);
-#if defined(RR_DIAG_NO_NONFINITE)  // diagnostic build only
-    const bool nf = false;
-#else
     const bool nf = nonfinite<NS>(y1);
-#endif
     bool bv;
     float t[NT];
     const float r = reward_terms<MODEL>(H, y1, a, v0, bv, t);
@@ -1294,20 +1195,12 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     ret += r;
     float o[NS];
     normalize_obs<NS>(y1, H.inv_norm, o);
-#if defined(RR_DIAG_STAMPS)
-    __builtin_amdgcn_sched_barrier(0);
-    dg_c[2] = (uint32_t)__builtin_amdgcn_s_memtime();
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    RR_STAMP(2);
 
     // Done compaction: one ballot per wave; lane 0 stores the wave's 64-bit done mask
     // (every wave writes its word each step, so no clearing and no atomics; the host
     // side expands the masks into the sorted index list, rr_fetch_done).
-#if defined(RR_DIAG_NO_DONE_TAIL)  // diagnostic build only: done lanes take no terminal-row / reset path
-    const bool dv = false;
-#else
     const bool dv = done && valid;
-#endif
     const uint64_t m = __ballot(dv);
     if (lane == 0) B.done_bits[wave_idx] = m;
     if (m) {
@@ -1347,10 +1240,8 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
     cw = CL.with_elapsed(cw, el);
 
     if (valid) {
-#if !defined(RR_DIAG_NO_STATE_STORE)  // diagnostic build only: the 14 state planes are not stored
 #pragma unroll
         for (int j = 0; j < NS; ++j) bst_f<SA>(st_r, y1[j], vo, j * plane);
-#endif
         if (use_counter) bst_u<SA>(st_r, cw, vo, (NS + 1) * plane);
         if (mode & RR_FLAG_EPISODE_STATS) bst_f<SA>(st_r, ret, vo, (NS + 2) * plane);
         store_outputs<NT, !ROWS>(io, i, vo, plane, n, r, done, trunc, t, bv, event ? 1.0f : (nf ? -1.0f : 0.0f));
@@ -1365,47 +1256,13 @@ __global__ __launch_bounds__(HELP ? 2 * WPB * kWave : WPB * kWave) __attribute__
         store_obs_tile<OW, kWave>(lds[wv], ow, make_rsrc(io.obs, (uint64_t)OW * plane), wave_base, lane, nvalid,
                                   io.obs_vec_ok);
     } else {
-    #if defined(RR_AB_OBS_DIRECT)  // A/B: obs rows stored from registers as 16-B pieces (no LDS tile)
-        if (valid) {
-            const rsrc_t orr = make_rsrc(io.obs, (uint64_t)NS * plane);
-            const uint32_t ro = NS == 14 ? (i << 6) - (i << 3) : i * (NS * 4u);
-#pragma unroll
-            for (int j = 0; j + 4 <= NS; j += 4)
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(o[j]), __float_as_uint(o[j + 1]),
-                                                             __float_as_uint(o[j + 2]), __float_as_uint(o[j + 3])},
-                                                       orr, (int)(ro + j * 4), 0, kOutAux);
-            if constexpr (NS % 4 == 2)
-                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, orr,
-                                                      (int)(ro + (NS - 2) * 4), 0, kOutAux);
-            else if constexpr (NS % 4 == 3)
-                __builtin_amdgcn_raw_buffer_store_b96(
-                    u32x3{__float_as_uint(o[NS - 3]), __float_as_uint(o[NS - 2]), __float_as_uint(o[NS - 1])}, orr,
-                    (int)(ro + (NS - 3) * 4), 0, kOutAux);
-        }
-#elif defined(RR_AB_VEC_MODE)
-        store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
-                                  (mode & kModeObsVec) != 0u);
-#elif defined(RR_DIAG_NO_OBS_STORE)  // diagnostic build only: no obs tile / stores
-        (void)nvalid;
-#else
         store_obs_tile<NS, kWave>(lds[wv], o, make_rsrc(io.obs, (uint64_t)NS * plane), wave_base, lane, nvalid,
                                   io.obs_vec_ok);
-#endif
     }
-#if defined(RR_DIAG_STAMPS)
     // lanes 0..2: barrier / loads / compute cycles; 3: the tail (outputs issued); 4, 5: the wave's
     // s_memrealtime start / end (100 MHz, low 32 bits, bit patterns in the float slots)
-    __builtin_amdgcn_sched_barrier(0);
-    dg_c[3] = (uint32_t)__builtin_amdgcn_s_memtime();
-    const uint32_t dg_rt1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    float dv_ = (float)(dg_c[0] - dg_c0);
-    dv_ = lane == 1 ? (float)(dg_c[1] - dg_c[0]) : dv_;
-    dv_ = lane == 2 ? (float)(dg_c[2] - dg_c[1]) : dv_;
-    dv_ = lane == 3 ? (float)(dg_c[3] - dg_c[2]) : dv_;
-    dv_ = lane == 4 ? __uint_as_float((uint32_t)dg_rt0) : dv_;
-    dv_ = lane == 5 ? __uint_as_float(dg_rt1) : dv_;
-    if (lane < 6 && valid) io.reward[i] = dv_;
-#endif
+    RR_STAMP(3);
+    RR_STAMPS_WRITE(io.reward, i, lane, valid, true);
 }
 
 template <int MODEL>
@@ -1685,21 +1542,21 @@ KParams make_kparams(const rr_params& p)
     const double pi = 3.14159265358979323846;
     for (int ax = 0; ax < 3; ++ax) {
         const double L = p.att_limit[ax], M = p.land_att_limit[ax];
+        // limits outside the angle's range make a test constant: |e| > L always holds for L < 0
+        // (threshold 2 on axes 0 / 2: X < 2r for every r > 0, since |X| <= r; -1 on axis 1: |S| > -1;
+        // the one exception, r == 0 exactly — the pitch singularity — reads false), and |e| < M
+        // never holds for M <= 0 (X > 2r and |S| < -1 are never true)
         if (ax == 1) {  // b = asin(R02) in [-pi/2, pi/2]
             if (L >= pi / 2) k.att_never |= 1u << ax;
-            else k.att_c[ax] = (float)std::sin(L);
+            else k.att_c[ax] = L < 0 ? -1.0f : (float)std::sin(L);
             if (M > pi / 2) k.land_always |= 1u << ax;
-            else k.land_c[ax] = (float)std::sin(M);
+            else k.land_c[ax] = M <= 0 ? -1.0f : (float)std::sin(M);
         } else {        // a, c = atan2(.) in [-pi, pi]
             if (L >= pi) k.att_never |= 1u << ax;
-            else k.att_c[ax] = (float)std::cos(L);
+            else k.att_c[ax] = L < 0 ? 2.0f : (float)std::cos(L);
             if (M > pi) k.land_always |= 1u << ax;
-            else k.land_c[ax] = (float)std::cos(M);
+            else k.land_c[ax] = M <= 0 ? 2.0f : (float)std::cos(M);
         }
-#if defined(RR_AB_REWARD2)
-        k.att_cs[ax] = k.att_c[ax] * std::fabs(k.att_c[ax]);
-        k.land_cs[ax] = k.land_c[ax] * std::fabs(k.land_c[ax]);
-#endif
     }
     k.omega_lt = ceil_f(p.omega_lim[0]);
     k.zero_h = floor_f(1e-3);
@@ -1740,6 +1597,9 @@ XParams make_xparams(const rr_params& p)
         const double pi = 3.14159265358979323846;
         for (int ax = 0; ax < 3; ++ax) {  // as make_kparams' float thresholds, in fp64
             const double L = p.att_limit[ax], M = p.land_att_limit[ax];
+            // constant tests: |e| > L for L < 0 always, |e| < M for M <= 0 never (finish6)
+            if (L < 0) x.att_always |= 1u << ax;
+            if (M <= 0) x.land_never |= 1u << ax;
             if (ax == 1) {
                 if (L >= pi / 2) x.att_never |= 1u << ax;
                 else x.att_c[ax] = std::sin(L);
@@ -1787,13 +1647,32 @@ struct rr_env {
     float* g_ret;
     int32_t* g_len;
     uint8_t* g_trunc;   // rr_gather_rows scratch
-    // the stream of the last launch that reads the reset-stream key (step, reset, rollout kernels):
-    // rr_seed on another stream first waits for the device (a stored handle, never dereferenced)
-    void* last_stream;
-    bool launched;
+    // the streams the handle's key-reading launches (step, reset, rollout kernels) were queued on,
+    // most recent last (stored handles, compared only): rr_seed makes its key copy wait for the work
+    // queued on each of them (seed_ev), and for the whole device past kSeedStreams distinct streams
+    static constexpr int kSeedStreams = 8;
+    void* streams[kSeedStreams];
+    int n_streams;
+    bool streams_overflow;
+    hipEvent_t seed_ev;
 };
 
 namespace {
+
+// note that a launch reading the reset-stream key went to `stream` (rr_seed orders its key copy after
+// the work queued on every stream noted): a pointer compare per launch, no HIP call
+inline void note_stream(rr_env* e, void* stream)
+{
+    if (e->n_streams > 0 && e->streams[e->n_streams - 1] == stream) return;
+    for (int k = 0; k < e->n_streams; ++k)
+        if (e->streams[k] == stream) {
+            for (int j = k; j + 1 < e->n_streams; ++j) e->streams[j] = e->streams[j + 1];
+            e->streams[e->n_streams - 1] = stream;
+            return;
+        }
+    if (e->n_streams < rr_env::kSeedStreams) e->streams[e->n_streams++] = stream;
+    else e->streams_overflow = true;
+}
 
 Bufs bufs_of(const rr_env* e)
 {
@@ -1934,6 +1813,7 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->kp.id_off = env_id_offset;
     {
         hipError_t err = hipMalloc((void**)&e->d_kp, sizeof(KParams));
+        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->seed_ev, hipEventDisableTiming);
         if (err == hipSuccess) err = hipMalloc((void**)&e->d_xp, sizeof(XParams));
         if (err == hipSuccess) err = hipMemcpy(e->d_xp, &e->xp, sizeof(XParams), hipMemcpyHostToDevice);
         if (err != hipSuccess) {
@@ -1962,6 +1842,7 @@ int rr_destroy(rr_env* e)
         (void)hipHostFree(e->state);
         e->state = nullptr;
     }
+    if (e->seed_ev) (void)hipEventDestroy(e->seed_ev);
     void* ptrs[] = {e->state, e->state64, e->d_kp, e->d_xp, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len,
                     e->g_trunc};
@@ -1993,13 +1874,35 @@ int rr_seed(rr_env* e, uint64_t seed, void* stream)
     if (cs != hipStreamCaptureStatusNone)
         return fail(RR_EINVAL, "rr_seed: the stream is being captured into a graph (seed before capturing: "
                                "replays read the key current when they run)");
-    // a launch of this handle queued on ANOTHER stream may still read the key: the new key must not
-    // land under it. Only then the device is synchronised; the usual single-stream
-    // caller keeps the stream-ordered write.
-    if (e->launched && e->last_stream != stream) {
-        err = hipDeviceSynchronize();
-        if (err != hipSuccess) return hip_fail(err, "rr_seed: synchronise the handle's earlier stream");
+    // launches of this handle queued on OTHER streams may still read the key: the new key must not
+    // land under them. The copy waits, on the device, for the work queued so far on
+    // every stream the handle launched on (the per-handle event recorded there now); the usual
+    // single-stream caller keeps the plain stream-ordered write. Past kSeedStreams distinct streams
+    // the device is synchronised. A stream being captured has run nothing of the capture yet.
+    // Graph replays are not launches of the handle: the caller orders them (header).
+    // A noted stream the runtime no longer knows (destroyed since: its queued work still runs) is
+    // covered by the same device synchronise.
+    bool sync_device = e->streams_overflow;
+    for (int k = 0; k < e->n_streams && !sync_device; ++k) {
+        hipStream_t o = (hipStream_t)e->streams[k];
+        if (o == s) continue;
+        hipStreamCaptureStatus ocs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(o, &ocs) != hipSuccess) {
+            (void)hipGetLastError();
+            sync_device = true;
+            break;
+        }
+        if (ocs != hipStreamCaptureStatusNone) continue;
+        err = hipEventRecord(e->seed_ev, o);
+        if (err == hipSuccess) err = hipStreamWaitEvent(s, e->seed_ev, 0);
+        if (err != hipSuccess) return hip_fail(err, "rr_seed: order the key after the handle's other streams");
     }
+    if (sync_device) {
+        err = hipDeviceSynchronize();
+        if (err != hipSuccess) return hip_fail(err, "rr_seed: synchronise the device");
+    }
+    e->n_streams = 0;  // everything queued so far is ordered before the key copy
+    e->streams_overflow = false;
     seed_words(seed, e->kp.seed_w);
     err = hipMemcpyAsync(e->d_kp, &e->kp, sizeof(KParams), hipMemcpyHostToDevice, s);
     if (err == hipSuccess) err = hipStreamSynchronize(s);  // e->kp is pageable host memory: wait until it is read
@@ -2017,8 +1920,7 @@ int rr_reset(rr_env* e, const uint8_t* mask, float* obs, void* stream)
         hipLaunchKernelGGL(reset_kernel<3>, dim3(grid_of(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->kp, b,
                            mask, obs, e->state64);
     hipError_t err = hipGetLastError();
-    e->last_stream = stream;
-    e->launched = true;
+    note_stream(e, stream);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_reset: launch");
 }
 
@@ -2039,11 +1941,6 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     io.terms = terms;
     io.obs_vec_ok = ((uintptr_t)obs & 15u) == 0;
     const Bufs b = bufs_of(e);
-#if defined(RR_AB_VEC_MODE)
-    const uint32_t vec_mode = io.obs_vec_ok ? kModeObsVec : 0u;
-#else
-    const uint32_t vec_mode = 0u;
-#endif
     hipStream_t s = (hipStream_t)stream;
     const bool m6 = e->p.model == RR_MODEL_6DOF;
     const bool euler = e->p.integrator == RR_INT_EULER;
@@ -2059,7 +1956,7 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
         const uint32_t nn = (uint32_t)e->n;
         const bool counter = e->p.max_episode_steps > 0 || (e->p.flags & (RR_FLAG_EPISODE_STATS | RR_FLAG_AUTO_RESET));
         const uint32_t mode =
-            e->p.flags | (counter ? kModeCounter : 0u) | (e->n > e->whole_line_min_n ? kModeWholeLines : 0u) | vec_mode;
+            e->p.flags | (counter ? kModeCounter : 0u) | (e->n > e->whole_line_min_n ? kModeWholeLines : 0u);
         const bool soa = e->p.flags & RR_FLAG_ACTION_SOA;
         // small N (at most ~2 main waves per SIMD): helper waves draw the reset candidates
         const bool help = (mode & RR_FLAG_AUTO_RESET) && e->n <= e->help_max_n;
@@ -2101,8 +1998,7 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return hip_fail(err, "rr_step: launch");
     e->steps++;
-    e->last_stream = stream;
-    e->launched = true;
+    note_stream(e, stream);
     return RR_OK;
 }
 }  // namespace
@@ -2572,8 +2468,7 @@ int launch_rollout(rr_env* e, const char* who, bool multi, const float* params, 
     }
     if (err != hipSuccess) return hip_fail(err, (std::string(who) + ": launch").c_str());
     e->steps += io.T;
-    e->last_stream = stream;
-    e->launched = true;
+    note_stream(e, stream);
     return RR_OK;
 }
 }  // namespace

@@ -167,3 +167,41 @@ def test_ppo_replicas_allreduce_world2_gloo():
     torch.optim.Adam(ref.parameters(), lr=3e-4, eps=1e-5).step()
     for a, b in zip(res[0], ref.parameters()):
         np.testing.assert_allclose(a, b.detach().numpy(), atol=1e-6, rtol=1e-5)
+
+
+def _rank_rows_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import per_rank_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["LOCAL_RANK"] = str(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows = per_rank_rows(dist, 0.1 * (rank + 1), 0.004 * (rank + 1), 20)  # rank r: (r + 1) x the wall / device time
+    q.put((rank, rows))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_per_rank_rows_world4_gloo():
+    """at world > 1 the bench line carries every rank's own wall time and events
+    figure (one all_gather_object), not only rank 0's and the max; a 4-rank rehearsal shows four
+    entries, in rank order, identical on every rank."""
+    world = 4
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        rows = got[r]
+        assert [x["rank"] for x in rows] == list(range(world)) and rows == got[0]
+        for k, x in enumerate(rows):
+            assert abs(x["wall_ms_per_step"] - 5.0 * (k + 1)) < 1e-9
+            assert abs(x["kernel_us"] - 4.0 * (k + 1)) < 1e-9 and x["local_rank"] == k

@@ -240,3 +240,15 @@ def test_exact_auto_reset_time_limit():
     np.testing.assert_allclose(obs.cpu().numpy(), (st.T / cfg.state_normalizer).astype(np.float32), rtol=1e-6,
                                atol=1e-7)
     b.close()
+
+
+def test_exact_negative_attitude_limits(oracle_mod, lean):
+    """The exact kernel's constant attitude tests (XParams att_always / land_never for limits below 0):
+    penalty and landing bonus row for row with the oracle's atan2 / asin, both exact kernels."""
+    from test_gpu_parity import _negative_limit_rows
+
+    n = 4096
+    ic, s, a, kw, ref = _negative_limit_rows(oracle_mod, n, 9)
+    out = run_exact(6, dict(ic=ic, state_in=s, action=a, t_in=np.zeros(n)), **kw)
+    assert np.array_equal(out["terms"][:, 3] != 0, ref["terms"][:, 3] != 0)
+    assert np.array_equal(out["terms"][:, 4] != 0, ref["terms"][:, 4] != 0)

@@ -468,3 +468,34 @@ def test_small_and_ragged_batches(model, n, golden6, golden3):
     assert np.array_equal(out["done"], rows["done"])
     for k in ("state_out", "obs", "reward", "terms"):
         assert np.array_equal(out[k], full[k][sel]), k
+
+
+NEG_ATT = (-0.1, -0.2, 1.0)   # attitude penalty limits below 0: |angle| > limit holds for every row
+NEG_LAND = (-0.1, 0.0, 0.3)   # landing limits <= 0 never admit; the landing's any() hinges on axis 2
+
+
+def _negative_limit_rows(oracle_mod, n, seed):
+    """Rows that touch down (_near_limit_landing_rows6), with attitude / landing limits outside the
+    angles' range (NEG_ATT, NEG_LAND; rocket_env.py:852-855, 1040-1061 compare |angle| with the
+    configured limit, whatever its sign), and the oracle's step of them."""
+    import copy
+    ic, s, a, axis, d = _near_limit_landing_rows6(n, seed, -3.0, -1.0)
+    s = s.astype(np.float32).astype(np.float64)
+    kw = copy.deepcopy(oracle_mod.ENV_CONFIG_6DOF)
+    kw["trajectory_limits"]["attitude_limit"] = list(NEG_ATT)
+    kw["landing_params"]["landing_attitude_limit"] = list(NEG_LAND)
+    ref = oracle_mod.step(oracle_mod.make_cfg(6, **kw), ic, 0.0, s, a, nthreads=8)
+    assert (ref["terms"][:, 3] != 0).all()  # the penalty on every row
+    landed = ref["terms"][:, 4] != 0
+    assert 0.05 < landed.mean() < 0.5 and not landed[axis != 2].any()
+    return ic, s, a, kw, ref
+
+
+def test_negative_attitude_limits_fast(oracle_mod):
+    """Limits outside the angles' range make the attitude tests constant (make_kparams' thresholds):
+    the attitude penalty and the landing bonus agree with the oracle's atan2 / asin row for row."""
+    n = 4096
+    ic, s, a, kw, ref = _negative_limit_rows(oracle_mod, n, 8)
+    out = run_rows(6, dict(group=np.zeros(n, np.int8), ic=ic, state_in=s, action=a), **kw)
+    assert np.array_equal(out["terms"][:, 3] != 0, ref["terms"][:, 3] != 0)
+    assert np.array_equal(out["terms"][:, 4] != 0, ref["terms"][:, 4] != 0)

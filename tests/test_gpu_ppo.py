@@ -278,3 +278,31 @@ def test_fused_update_refuses_a_one_row_remainder_before_stepping():
     assert all(abs(v) < 1e9 for v in stats.values())
     assert any(not torch.equal(a, b) for a, b in zip(before, pol.parameters()))
     env.close()
+
+
+def test_rollout_and_learner_forwards_agree():
+    """The fp32 rollout runs the tanh FOLDED into its packed weights (rocket_policy.inc kPolFoldTanh,
+    include/rocket_hip.h RR_POLICY_FP32); the learner (rr_ppo_grad) packs and runs the unfolded
+    tanh. On the same parameters and the rollout's own samples the two forwards agree to rounding,
+    not bit for bit: with old_log_prob = the rollout's log_prob and returns = the rollout's values,
+    rr_ppo_grad's approx_kl (mean (r - 1) - log r) is ~0, no ratio is clipped, and its value loss
+    (the mean squared gap between the two value forwards) is ~0. Bars: approx_kl <= 1e-9 (a log-prob
+    gap of ~4e-5), rms value gap <= 1e-5 x (1 + rms value)."""
+    import torch
+    from rl_rocket_amd.rollout import PPOGrad
+
+    env, pol, ro = _rollout_for_update(n=8192, T=8, seed=9)
+    n = ro.n_steps * env.num_envs
+    ro_cmp = types.SimpleNamespace(n_steps=ro.n_steps, env=ro.env, obs=ro.obs, actions=ro.actions,
+                                   log_probs=ro.log_probs, advantages=ro.advantages, returns=ro.values.clone())
+    grad = PPOGrad(pol, ro_cmp, n)
+    idx = torch.arange(n, device="cuda:0", dtype=torch.int64)
+    pl, vl, ent, clip_frac, approx_kl = grad(idx).tolist()
+    torch.cuda.synchronize()
+    rms_v = ro.values.double().pow(2).mean().sqrt().item()
+    print("approx_kl %.3e clip_fraction %.3g rms value gap %.3e (rms value %.3f)" % (approx_kl, clip_frac, vl ** 0.5,
+                                                                                 rms_v))
+    assert clip_frac == 0.0
+    assert abs(approx_kl) <= 1e-9
+    assert vl ** 0.5 <= 1e-5 * (1.0 + rms_v)
+    env.close()

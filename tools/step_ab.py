@@ -1,6 +1,8 @@
 """A/B timing of step-kernel builds: the production library against diagnostic and candidate
-builds of the same source (compile-time macros RR_DIAG_* / RR_AB_*, libraries under tools/ab/,
-built beforehand in this container with rl_rocket_amd.build.build_lib(out, defines=[...])).
+builds (libraries under tools/ab/, built beforehand in this container with
+rl_rocket_amd.build.build_lib(out, defines=[...]) from edited copies of the sources). The round-5
+apportionment's RR_DIAG_NO_* / RR_AB_* variants were deleted from csrc/ in round 6 (they live in
+git history at 1ad310c); only RR_DIAG_STAMPS (rocket_stamps.h) stays in the source.
 
     python tools/step_ab.py run --libs base,d_notrans,ab_reward2 [--reps 2] [--n 65536] --out FILE
     python tools/step_ab.py one --lib tools/ab/lib_base.so [--n 65536]      (one library, one process)
