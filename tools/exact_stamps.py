@@ -51,10 +51,18 @@ def main():
            "total_median": float(np.median(tot)), "total_p90": float(np.percentile(tot, 90)), "phases": {}}
     for p, name in enumerate(PHASES):
         out["phases"][name] = {"median": float(np.median(x[:, p])), "p10": float(np.percentile(x[:, p], 10)),
-                               "p90": float(np.percentile(x[:, p], 90)), "max": float(x[:, p].max())}
+                               "p90": float(np.percentile(x[:, p], 90)), "p99": float(np.percentile(x[:, p], 99)),
+                               "max": float(x[:, p].max())}
         print("%-22s median %8.0f  p10 %8.0f  p90 %8.0f  max %8.0f" % (
             name, out["phases"][name]["median"], out["phases"][name]["p10"], out["phases"][name]["p90"],
             out["phases"][name]["max"]))
+    # the launch is set by its slowest wave: per step, the slowest wave's total and where it went
+    w = a.n // 64
+    per_step = x.reshape(a.reps, w, 4)
+    slow = per_step.sum(axis=2).argmax(axis=1)
+    out["slowest_wave_per_step"] = [[float(v) for v in per_step[r, slow[r]]] for r in range(a.reps)]
+    out["cp_max"] = os.environ.get("RR_EXACT_CP_MAX")
+    print("slowest wave per step (phases, cycles):", out["slowest_wave_per_step"])
     print("total median %.0f p90 %.0f cycles" % (out["total_median"], out["total_p90"]))
     if a.out:
         os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)

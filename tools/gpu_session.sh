@@ -35,6 +35,8 @@ fi
 if has dist; then
   (export RR_BENCH_ONE_DEVICE=1 RR_BENCH_BACKEND=gloo; step bench_gpus2_gloo 400 $B --gpus 2 --steps 20 --warmup 5 > "$OUT/bench_gpus2_gloo.json" 2> "$OUT/bench_gpus2_gloo.err") || exit $?
   cat "$OUT/bench_gpus2_gloo.json"
+  # configs[3]'s launcher path at 4 ranks: the line's per_rank rows (every rank's wall / events figure)
+  (export RR_BENCH_ONE_DEVICE=1 RR_BENCH_BACKEND=gloo; step bench_gpus4_gloo 400 $B --gpus 4 --steps 20 --warmup 5 > "$OUT/bench_gpus4_gloo.json" 2> "$OUT/bench_gpus4_gloo.err") || exit $?
   step bench_gather_w1 300 $B --gather-leg --steps 20 --warmup 5 --no-cpu-baseline --no-sb3-legs > "$OUT/bench_gather_w1.json" 2> "$OUT/bench_gather_w1.err"
 fi
 export TMPDIR=/tmp
