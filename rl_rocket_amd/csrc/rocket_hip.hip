@@ -1738,13 +1738,6 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
     e->p = *p;
     e->kp = make_kparams(*p);
     e->xp = make_xparams(*p);
-    {
-        // exact mode's straggler threshold: a wave continues its last envs component-parallel
-        // once at most one batch of them (4 6DOF envs on 16 lanes each, 8 3DOF envs on 8) is still
-        // stepping; RR_EXACT_CP_MAX overrides it (0: the lane-per-env loop to the end)
-        const char* cv = std::getenv("RR_EXACT_CP_MAX");
-        e->xp.cp_max = cv ? (int32_t)std::strtol(cv, nullptr, 10) : (p->model == RR_MODEL_6DOF ? 4 : 8);
-    }
     e->ns = p->model == RR_MODEL_6DOF ? 14 : 7;
     e->na = p->model == RR_MODEL_6DOF ? 3 : 2;
     e->nt = p->model == RR_MODEL_6DOF ? 5 : 6;

@@ -253,57 +253,3 @@ def test_exact_negative_attitude_limits(oracle_mod, lean):
     assert np.array_equal(out["terms"][:, 3] != 0, ref["terms"][:, 3] != 0)
     assert np.array_equal(out["terms"][:, 4] != 0, ref["terms"][:, 4] != 0)
 
-
-def _exact_trajectory(model, n, steps, action_seed, **kw):
-    """`steps` exact steps of n envs under TimeLimit 40 + auto-reset from seeded random actions; every
-    output of every step, bitwise comparable."""
-    import torch
-    from rl_rocket_amd.batch import RocketBatch
-
-    b = RocketBatch(n, model=model, device="cuda:0", integrator="dopri5", max_episode_steps=40, auto_reset=True,
-                    compute_terms=True, **kw)
-    b.reset()
-    g = torch.Generator(device="cuda:0").manual_seed(action_seed)
-    outs = []
-    for _ in range(steps):
-        a = torch.rand((n, b.action_dim), device="cuda:0", generator=g) * 2 - 1
-        obs, rew, done, trunc = b.step(a)
-        outs.append([x.clone() for x in (obs, rew, done, trunc, b.terms)])
-    outs.append(list(b.get_state64()) + list(b.get_state()))
-    torch.cuda.synchronize()
-    b.close()
-    return outs
-
-
-@pytest.mark.parametrize("model", [6, 3])
-@pytest.mark.parametrize("cp_max", ["64", "4"])
-def test_straggler_pass_is_bitwise_one_pass(model, cp_max, lean, monkeypatch, oracle_mod):
-    """a wave's last stepping envs continue component-parallel (solve_cp: GL lanes
-    per env, the RHS on the gathered vector, the error sum in component order). Every output is
-    bitwise the lane-per-env loop's (RR_EXACT_CP_MAX=0): on 65 536 seeded rows with ground events
-    (each step of the oracle's own kind), and over 30 auto-reset steps of a batch (TimeLimit 40:
-    resets, events, bounds). cp_max 64 hands EVERY env with a second step to the component-parallel
-    path (16 batches per wave), 4 is the default."""
-    import torch
-    from test_gpu_parity import _random_states3, _random_states6
-
-    n = 65536
-    ic, s, a = (_random_states6 if model == 6 else _random_states3)(n, seed=21)
-    rows = dict(ic=ic, state_in=s, action=a, t_in=np.zeros(n))
-    monkeypatch.setenv("RR_EXACT_CP_MAX", "0")
-    ref = run_exact(model, rows, **_kw(model))
-    ref_t = _exact_trajectory(model, 20003, 30, 5, **_kw(model))
-    monkeypatch.setenv("RR_EXACT_CP_MAX", cp_max)
-    out = run_exact(model, rows, **_kw(model))
-    out_t = _exact_trajectory(model, 20003, 30, 5, **_kw(model))
-    assert ref["event"].sum() > 100
-    for k in ("state_out", "state32", "obs", "reward", "terms", "done", "bounds_violation", "event"):
-        assert np.array_equal(out[k], ref[k], equal_nan=out[k].dtype.kind == "f"), k
-    for t, (x, y) in enumerate(zip(out_t, ref_t)):
-        for u, v in zip(x, y):
-            assert torch.equal(u, v) or (u.is_floating_point() and torch.equal(u.isnan(), v.isnan()) and
-                                         torch.equal(u[~u.isnan()], v[~v.isnan()])), t
-    # and the component-parallel result is the oracle's (the rows' own bar)
-    cfg = oracle_mod.make_cfg(model, **(oracle_mod.ENV_CONFIG_6DOF if model == 6 else oracle_mod.DEFAULTS_3DOF))
-    o = oracle_mod.step(cfg, ic, 0.0, s, a, nthreads=8)
-    assert np.array_equal(out["event"], o["status"] == 1) and np.array_equal(out["done"], o["done"])
