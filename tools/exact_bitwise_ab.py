@@ -64,7 +64,7 @@ def run_one(out, n, steps, lean):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--libs", required=True)
+    ap.add_argument("--libs")
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--lean", action="store_true")
