@@ -1186,6 +1186,10 @@ def main():
                 "ms_per_step": r_i["dt"] / K * 1e3, "kernel_us": r_i["kern_ms"] * 1e3,
                 "frac": b_i / (r_i["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "frac_wall": b_i / (r_i["dt"] / K) / 1e9 / HBM_PEAK_GBS})
+            if r_i.get("per_rank"):
+                walls = [r["wall_ms_per_step"] for r in r_i["per_rank"]]
+                result["n_sweep"][-1]["per_rank"] = r_i["per_rank"]
+                result["n_sweep"][-1]["per_rank_wall_max_over_min"] = max(walls) / min(walls)
             e_i.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baselines(model, args.cpu_seconds, host_cores())
