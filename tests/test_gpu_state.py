@@ -324,6 +324,46 @@ def test_reseed_applies_to_graphs_captured_before(model, n, help_max, monkeypatc
     assert not torch.equal(a.get_state()[0], c.get_state()[0])  # the key changed the resets
 
 
+def test_seed_between_replays_on_another_stream():
+    """a graph captured on stream S and replayed on stream R is not a launch of the handle,
+    so rr_seed does not track it (include/rocket_hip.h); the documented protocol — order the replay
+    before the seed (here: synchronise R) — gives the first replay the old key and the second the new
+    one, bitwise an eager twin that seeds between the same steps."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+
+    n = 20003
+    mk = lambda: RocketBatch(n, model=6, device="cuda:0", max_episode_steps=2, **_env6())  # noqa: E731
+    a, b = mk(), mk()
+    for e in (a, b):
+        e.reset()
+    acts = _actions(n, 3, 4, 33)
+    cap, rep = torch.cuda.Stream(), torch.cuda.Stream()
+    cap.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(cap):
+        with torch.cuda.graph(g, stream=cap):
+            for act in acts:
+                b.step(act)
+    torch.cuda.synchronize()
+    rep.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(rep):
+        g.replay()
+    rep.synchronize()  # the caller orders the replay before the seed
+    b.seed(4242)
+    with torch.cuda.stream(rep):
+        g.replay()
+    for act in acts:
+        a.step(act)
+    a.seed(4242)
+    for act in acts:
+        a.step(act)
+    torch.cuda.synchronize()
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward)
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
+
+
 def test_elapsed_saturates_past_the_time_limit():
     """without auto-reset a finished env keeps stepping; its elapsed field saturates
     at 2^E - 1 (E = 3 bits for TimeLimit 5) instead of wrapping into the episode field, so
