@@ -225,50 +225,55 @@ class Rocket6DOF(_RocketBase):
 
         return pd.DataFrame(self.vtarg_history, columns=["v_x", "v_y", "v_z"])
 
-    # -- episode figures read by EpisodeAnalyzer (rocket_env.py:861-950; plotly imported lazily) ----------------
+    # -- episode figures read by EpisodeAnalyzer (rocket_env.py:861-950) ------------------------------------
+    # The reference's three figures (3D path with velocity cones over the landing pad, 3D path with the
+    # target-velocity field and the landing target, the quaternion's components over time), built here by
+    # one helper on plotly.graph_objects (imported lazily: plotting is off the step path).
     @staticmethod
-    def _plotly():
+    def _go():
         try:
-            import plotly.express as px
+            import plotly.graph_objects as go
         except ImportError as e:  # pragma: no cover - plotly ships with this image
             raise ImportError("the episode figures (get_trajectory_plotly & co.) need plotly") from e
-        return px
+        return go
 
-    def _trajectory_plot_from_df(self, df):
-        """3D trajectory, landing pad disc (radius target_r at x = 0) and velocity cones."""
-        px = self._plotly()
-        fig = px.line_3d(df[["x", "y", "z"]], x="x", y="y", z="z")
-        g = np.linspace(-self.target_r, self.target_r, 100)
-        zv, yv = np.meshgrid(g, g)
-        pad = 1.0 * (zv ** 2 + yv ** 2 < self.target_r ** 2)
-        fig.add_surface(x=pad, y=yv, z=zv, surfacecolor=pad, showscale=False)
-        fig.add_cone(x=df["x"], y=df["y"], z=df["z"], u=df["vx"], v=df["vy"], w=df["vz"], sizeref=3)
-        fig.update_layout(scene_aspectmode="data")
-        return fig
-
-    def _vtarg_plot_figure(self, df):
-        """3D trajectory with the target-velocity field v_targ along it and the landing target."""
-        px = self._plotly()
-        vt = self.vtarg_to_dataframe()
-        k = min(len(df), len(vt))  # vtarg_history has one row per step, the states one more (the IC)
-        fig = px.line_3d(df[["x", "y", "z"]], x="x", y="y", z="z")
-        fig.update_layout(scene_camera=dict(up=dict(x=1, y=0, z=0), center=dict(x=0, y=0, z=0),
-                                            eye=dict(x=0.625, y=1.25, z=0.0)))
-        x_f, y_f, z_f = self.landing_target
-        fig.add_scatter3d(x=[x_f], y=[y_f], z=[z_f])
-        fig.add_cone(x=df["x"][:k], y=df["y"][:k], z=df["z"][:k], u=vt["v_x"][:k], v=vt["v_y"][:k], w=vt["v_z"][:k],
-                     sizeref=3)
+    def _path_figure(self, arrows, pad=False, target=False):
+        """The episode's 3D path (x altitude, y, z), `arrows` = (u, v, w) columns drawn as cones along
+        it, optionally the landing pad (a disc of radius target_r in the x = 0 plane) and the target."""
+        go = self._go()
+        df = self.states_to_dataframe()
+        u, v, w = (np.asarray(c, dtype=np.float64) for c in arrows)
+        k = min(len(df), len(u))  # vtarg rows: one per step; state rows: one more (the IC)
+        x, y, z = (df[c].to_numpy(dtype=np.float64) for c in ("x", "y", "z"))
+        traces = [go.Scatter3d(x=x, y=y, z=z, mode="lines", name="trajectory"),
+                  go.Cone(x=x[:k], y=y[:k], z=z[:k], u=u[:k], v=v[:k], w=w[:k], sizeref=3, showscale=False)]
+        if pad:
+            r = float(self.target_r)
+            ax = np.linspace(-r, r, 100)
+            zz, yy = np.meshgrid(ax, ax)
+            disc = (zz * zz + yy * yy < r * r).astype(np.float64)
+            traces.append(go.Surface(x=disc, y=yy, z=zz, surfacecolor=disc, showscale=False, name="landing pad"))
+        fig = go.Figure(data=traces)
+        if target:
+            tx, ty, tz = (float(c) for c in self.landing_target)
+            fig.add_trace(go.Scatter3d(x=[tx], y=[ty], z=[tz], mode="markers", name="target"))
+            fig.update_layout(scene_camera={"up": {"x": 1, "y": 0, "z": 0}, "center": {"x": 0, "y": 0, "z": 0},
+                                            "eye": {"x": 0.625, "y": 1.25, "z": 0.0}})
         fig.update_layout(scene_aspectmode="data")
         return fig
 
     def get_trajectory_plotly(self):
-        return self._trajectory_plot_from_df(self.states_to_dataframe())
-
-    def get_attitude_trajectory(self):
-        return self._plotly().line(self.states_to_dataframe()[["q0", "q1", "q2", "q3"]])
+        df = self.states_to_dataframe()
+        return self._path_figure((df["vx"], df["vy"], df["vz"]), pad=True)
 
     def get_vtarg_trajectory(self):
-        return self._vtarg_plot_figure(self.states_to_dataframe())
+        vt = self.vtarg_to_dataframe()
+        return self._path_figure((vt["v_x"], vt["v_y"], vt["v_z"]), target=True)
+
+    def get_attitude_trajectory(self):
+        go = self._go()
+        df = self.states_to_dataframe()
+        return go.Figure(data=[go.Scatter(x=df.index, y=df[c], mode="lines", name=c) for c in ("q0", "q1", "q2", "q3")])
 
     @property
     def rotation_obj(self):

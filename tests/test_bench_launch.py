@@ -95,8 +95,14 @@ def test_episode_analyzer_statistics_host():
     # the shim's figures (plotly is in this image)
     import plotly.graph_objects as go
 
-    assert isinstance(u.get_trajectory_plotly(), go.Figure)
-    assert isinstance(u.get_vtarg_trajectory(), go.Figure)
+    f = u.get_trajectory_plotly()
+    assert isinstance(f, go.Figure) and [t.type for t in f.data] == ["scatter3d", "cone", "surface"]
+    assert len(f.data[0].x) == len(u.SIM.states) and len(f.data[1].u) == len(u.SIM.states)
+    f = u.get_vtarg_trajectory()
+    assert [t.type for t in f.data] == ["scatter3d", "cone", "scatter3d"]
+    assert len(f.data[1].u) == len(u.SIM.states) - 1  # one target velocity per step
+    f = u.get_attitude_trajectory()
+    assert [t.name for t in f.data] == ["q0", "q1", "q2", "q3"]
 
 
 def test_host_cores_uses_the_affinity_mask_narrowed_by_quota_and_omp(monkeypatch):
