@@ -14,7 +14,7 @@ step() {  # step NAME TIMEOUT cmd...: 0 = ok, 1 = test failures (continue), anyt
   echo "[$name] start $(date +%T)" >&2
   timeout -k 10 "$to" "$@"
   local rc=$?
-  echo "[$name] exit $rc" | tee -a "$OUT/status.txt"
+  echo "[$name] exit $rc" >> "$OUT/status.txt"; echo "[$name] exit $rc" >&2
   if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
 }
 has() { case " $PHASES " in *" $1 "*) return 0;; esac; return 1; }
