@@ -70,11 +70,6 @@ constexpr int64_t kNarrowMaxN = 16384;
 // env per lane; above it the lean two-waves-per-SIMD kernel (rocket_dopri5.inc, solve LEAN). The
 // CU count is the device's (rr_create); kExactLeanCUs is the fallback if the query fails
 constexpr int64_t kExactLeanCUs = 256;
-// exact mode's straggler deferral (the lean kernel's two-launch step): on above this N (measured
-// slower at 524 288 and 4 194 304: off unless RR_EXACT_DEFER_MIN_N), pass 1 capped at this many
-// accepted steps per env
-constexpr int64_t kExactDeferMinN = INT64_MAX;
-constexpr long long kExactDeferCap = 2;
 constexpr int kWave = 64;
 constexpr int kBlock = 256;  // threads per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
@@ -1367,8 +1362,7 @@ __global__ __launch_bounds__(kBlock) void copy_done_rows_kernel(const uint64_t* 
 // Bufs / StepIO / XParams of the calling TU (same definitions, same layout).
 extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model, int variant, const void* xp,
                                                                         const void* bufs, const void* io,
-                                                                        double* state64, unsigned grid,
-                                                                        unsigned resume_grid, void* stream)
+                                                                        double* state64, unsigned grid, void* stream)
 {
     Bufs b;
     StepIO o;
@@ -1379,20 +1373,11 @@ extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model,
     // variant bit 0 = lean (6DOF above one wave per SIMD, the caller's choice): 256 registers, two
     // waves per SIMD hide each other's fp64 latency (147.6 vs 176.6 us at N = 524 288); otherwise the
     // in-loop dense output (no event re-derivation, no spills: 28.9 vs 32.1 us at 65 536,
-    // profiles/r04/ab_lean/). Bit 1 = [NA][N] action planes (RR_FLAG_ACTION_SOA). Bit 2 (6DOF lean
-    // only) = the straggler deferral: pass 1 over the grid, then pass 2 over `resume_grid` workgroups.
-    const bool lean = variant & 1, soa = variant & 2, defer = variant & 4;
+    // profiles/r04/ab_lean/). Bit 1 = [NA][N] action planes (RR_FLAG_ACTION_SOA).
+    const bool lean = variant & 1, soa = variant & 2;
 #define RR_LAUNCH_X(M, L, A) \
     hipLaunchKernelGGL((step_exact_kernel<M, L, A>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64)
-#define RR_LAUNCH_D(A)                                                                                              \
-    do {                                                                                                            \
-        hipLaunchKernelGGL((step_exact_defer_kernel<6, A>), dim3(grid), dim3(kBlock), 0, s, x, b, o, state64);      \
-        hipLaunchKernelGGL((step_exact_resume_kernel<6, A>), dim3(resume_grid), dim3(kBlock), 0, s, x, b, o, state64); \
-    } while (0)
-    if (model == RR_MODEL_6DOF && lean && defer) {
-        if (soa) RR_LAUNCH_D(true);
-        else RR_LAUNCH_D(false);
-    } else if (model == RR_MODEL_6DOF && lean) {
+    if (model == RR_MODEL_6DOF && lean) {
         if (soa) RR_LAUNCH_X(6, true, true);
         else RR_LAUNCH_X(6, true, false);
     } else if (model == RR_MODEL_6DOF) {
@@ -1402,7 +1387,6 @@ extern "C" __attribute__((visibility("hidden"))) int rrx_launch_exact(int model,
         if (soa) RR_LAUNCH_X(3, false, true);
         else RR_LAUNCH_X(3, false, false);
     }
-#undef RR_LAUNCH_D
 #undef RR_LAUNCH_X
     return (int)hipGetLastError();
 }
@@ -1449,8 +1433,7 @@ extern "C" __attribute__((visibility("hidden"))) int rrc_launch_collect(int mode
 // file alone, e.g. a tools/ A/B variant) make RR_INT_DOPRI5 steps and rr_rollout_collect fail loudly
 // instead of failing to load
 extern "C" __attribute__((weak, visibility("hidden"))) int rrx_launch_exact(int, int, const void*, const void*,
-                                                                          const void*, double*, unsigned, unsigned,
-                                                                          void*)
+                                                                          const void*, double*, unsigned, void*)
 {
     return (int)hipErrorInvalidDeviceFunction;
 }
@@ -1645,8 +1628,6 @@ struct rr_env {
     uint64_t steps;
     int64_t help_max_n;       // largest N stepped with helper waves (kHelpMaxN, RR_HELP_MAX_N env override)
     int64_t exact_lean_min_n; // 6DOF exact mode: lean kernel above this N (CUs x 256, RR_EXACT_LEAN_MIN_N)
-    bool exact_defer;         // 6DOF exact mode, lean kernel: the straggler deferral (two launches per step)
-    unsigned resume_grid;     // its pass-2 workgroups (one per CU), one list group each
     int64_t whole_line_min_n; // plain step kernels: whole-line done-path stores above this N (kWholeLineMinN,
                               // RR_WHOLE_LINE_MIN_N)
     float* state;
@@ -1658,9 +1639,6 @@ struct rr_env {
     float* term_ret;
     int32_t* term_len;
     double* state64;    // RR_INT_DOPRI5 only
-    double* defer_planes; // the straggler deferral's list (XParams.defer_*), exact_defer only
-    int32_t* defer_idx;
-    uint32_t* defer_ctl;
     bool host_state;    // RR_FLAG_HOST_STATE: `state` (+ v0, counter, ep_ret planes) is pinned host memory
     KParams* d_kp;      // device copy of kp (Bufs.kp)
     XParams* d_xp;      // device copy of xp (RR_INT_DOPRI5: step_exact_kernel reads it where it uses it)
@@ -1778,16 +1756,6 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
             cus = (int)kExactLeanCUs;
         const char* lv = std::getenv("RR_EXACT_LEAN_MIN_N");
         e->exact_lean_min_n = lv ? std::strtoll(lv, nullptr, 10) : (int64_t)cus * 4 * kWave;
-        // the lean kernel's straggler deferral above RR_EXACT_DEFER_MIN_N (default kExactDeferMinN),
-        // pass 1 stopping envs after RR_EXACT_DEFER_CAP accepted steps (default kExactDeferCap)
-        const char* dv = std::getenv("RR_EXACT_DEFER_MIN_N");
-        const char* cv = std::getenv("RR_EXACT_DEFER_CAP");
-        const int64_t defer_min_n = dv ? std::strtoll(dv, nullptr, 10) : kExactDeferMinN;
-        const long long cap = cv ? std::strtoll(cv, nullptr, 10) : kExactDeferCap;
-        e->exact_defer = p->integrator == RR_INT_DOPRI5 && p->model == RR_MODEL_6DOF && n > e->exact_lean_min_n &&
-                         n > defer_min_n && cap >= 0;
-        e->xp.defer_cap = (uint32_t)std::min<long long>(std::max<long long>(cap, 0), 0xFFFFFFFFll);
-        e->resume_grid = (unsigned)std::max(1, std::min(cus, (int)grid_of(n)));
         // the plain kernels' whole-line done path (tests run it at small N with RR_WHOLE_LINE_MIN_N=0)
         const char* wv = std::getenv("RR_WHOLE_LINE_MIN_N");
         e->whole_line_min_n = wv ? std::strtoll(wv, nullptr, 10) : kWholeLineMinN;
@@ -1839,27 +1807,6 @@ int rr_create(rr_env** out, const rr_params* p, int64_t n, int64_t env_id_offset
             return hip_fail(err, "rr_create: hipMalloc (fp64 state)");
         }
     }
-    if (e->exact_defer) {
-        // pass-1 workgroup b fills group b mod G (G = pass 2's workgroups), which holds every env of
-        // its workgroups in the worst case: [2 NS + 3][G x group_cap] fp64 planes, the env column and
-        // G zeroed counter pairs
-        const uint32_t groups = e->resume_grid;
-        const uint32_t group_cap = (grid_of(n) + groups - 1) / groups * (uint32_t)kBlock;
-        const size_t len = (size_t)groups * group_cap, ctl = sizeof(uint32_t) * groups * kDeferCtlStride;
-        e->xp.defer_groups = groups;
-        e->xp.defer_group_cap = group_cap;
-        hipError_t err = hipMalloc((void**)&e->defer_planes, sizeof(double) * (2 * e->ns + 3) * len);
-        if (err == hipSuccess) err = hipMalloc((void**)&e->defer_idx, sizeof(int32_t) * len);
-        if (err == hipSuccess) err = hipMalloc((void**)&e->defer_ctl, ctl);
-        if (err == hipSuccess) err = hipMemset(e->defer_ctl, 0, ctl);
-        if (err != hipSuccess) {
-            rr_destroy(e);
-            return hip_fail(err, "rr_create: hipMalloc (exact deferral list)");
-        }
-        e->xp.defer_planes = e->defer_planes;
-        e->xp.defer_idx = e->defer_idx;
-        e->xp.defer_ctl = e->defer_ctl;
-    }
     e->v0 = e->state + (size_t)e->ns * n;
     e->counter = reinterpret_cast<uint32_t*>(e->state + (size_t)(e->ns + 1) * n);
     e->ep_ret = e->state + (size_t)(e->ns + 2) * n;
@@ -1896,7 +1843,7 @@ int rr_destroy(rr_env* e)
         e->state = nullptr;
     }
     if (e->seed_ev) (void)hipEventDestroy(e->seed_ev);
-    void* ptrs[] = {e->state, e->state64, e->defer_planes, e->defer_idx, e->defer_ctl, e->d_kp, e->d_xp, e->done_bits,
+    void* ptrs[] = {e->state, e->state64, e->d_kp, e->d_xp, e->done_bits,
                     e->term_obs, e->term_ret, e->term_len, e->g_idx, e->g_obs,  e->g_ret, e->g_len,
                     e->g_trunc};
     for (void* q : ptrs)
@@ -2001,10 +1948,9 @@ int launch_step(rr_env* e, const float* action, float* obs, float* reward, uint8
     if (e->p.integrator == RR_INT_DOPRI5) {
         // the exact kernels live in the second translation unit (rocket_exact.hip: compiled with a
         // register-pressure-first scheduler, no scratch spills)
-        const int variant = (m6 && e->n > e->exact_lean_min_n ? 1 : 0) | ((e->p.flags & RR_FLAG_ACTION_SOA) ? 2 : 0) |
-                            (e->exact_defer ? 4 : 0);
+        const int variant = (m6 && e->n > e->exact_lean_min_n ? 1 : 0) | ((e->p.flags & RR_FLAG_ACTION_SOA) ? 2 : 0);
         const hipError_t xe = (hipError_t)rrx_launch_exact(m6 ? RR_MODEL_6DOF : RR_MODEL_3DOF, variant, e->d_xp, &b,
-                                                           &io, e->state64, grid.x, e->resume_grid, s);
+                                                           &io, e->state64, grid.x, s);
         if (xe != hipSuccess) return hip_fail(xe, "rr_step: exact launch");
     } else {
         const uint32_t nn = (uint32_t)e->n;

@@ -14,17 +14,13 @@ REWARD_TOL = 1e-7    # floored-relative |a-b|/max(|b|,1): reward / terms are ret
 OBS_TOL = 1e-7
 
 
-@pytest.fixture(params=["inloop", "lean", "defer"])
+@pytest.fixture(params=[False, True], ids=["inloop", "lean"])
 def lean(request, monkeypatch):
-    """Every 6DOF exact kernel: the in-loop dense output (N <= 65 536), the lean two-waves-per-SIMD
-    kernel (above it; RR_EXACT_LEAN_MIN_N=0 selects it at any N) in one pass, and the lean kernel's
-    two-launch straggler deferral (RR_EXACT_DEFER_CAP=1: pass 1 stops envs after one accepted step
-    and defers every ground event, pass 2 resumes them)."""
-    if request.param != "inloop":
+    """Both 6DOF exact kernels: the in-loop dense output (N <= 65 536) and the lean
+    two-waves-per-SIMD kernel (above it; RR_EXACT_LEAN_MIN_N=0 selects it at any N)."""
+    if request.param:
         monkeypatch.setenv("RR_EXACT_LEAN_MIN_N", "0")
-        monkeypatch.setenv("RR_EXACT_DEFER_MIN_N", "0")
-        monkeypatch.setenv("RR_EXACT_DEFER_CAP", "1" if request.param == "defer" else "-1")
-    return request.param != "inloop"
+    return request.param
 
 
 def _kw(model):
@@ -177,7 +173,6 @@ def test_exact_lean_kernel_is_bitwise_the_inloop_kernel(monkeypatch):
     rows = dict(ic=ic, state_in=s, action=a, t_in=np.zeros(n))
     ref = run_exact(6, rows, **_kw(6))
     monkeypatch.setenv("RR_EXACT_LEAN_MIN_N", "0")
-    monkeypatch.setenv("RR_EXACT_DEFER_CAP", "-1")
     out = run_exact(6, rows, **_kw(6))
     print("event rows", int(ref["event"].sum()), "done rows", int(ref["done"].sum()))
     assert ref["event"].sum() > 100
@@ -258,50 +253,3 @@ def test_exact_negative_attitude_limits(oracle_mod, lean):
     assert np.array_equal(out["terms"][:, 3] != 0, ref["terms"][:, 3] != 0)
     assert np.array_equal(out["terms"][:, 4] != 0, ref["terms"][:, 4] != 0)
 
-
-
-def _defer_outputs(monkeypatch, cap, n, steps):
-    """Every output of the lean kernel over seeded rows with ground events (one step) and an
-    auto-reset trajectory under TimeLimit 40: one pass (cap -1) or the two-launch deferral."""
-    import torch
-    from rl_rocket_amd.batch import RocketBatch
-    from test_gpu_parity import _random_states6
-
-    monkeypatch.setenv("RR_EXACT_LEAN_MIN_N", "0")
-    monkeypatch.setenv("RR_EXACT_DEFER_MIN_N", "0")
-    monkeypatch.setenv("RR_EXACT_DEFER_CAP", str(cap))
-    res = {}
-    ic, s, a = _random_states6(n, seed=31)
-    rows = run_exact(6, dict(ic=ic, state_in=s, action=a, t_in=np.zeros(n)), **_kw(6))
-    res.update(("rows_" + k, v) for k, v in rows.items())
-    b = RocketBatch(n, model=6, device="cuda:0", integrator="dopri5", max_episode_steps=40, auto_reset=True,
-                    compute_terms=True, **_kw(6))
-    b.reset()
-    g = torch.Generator(device="cuda:0").manual_seed(7)
-    for t in range(steps):
-        act = torch.rand((n, 3), device="cuda:0", generator=g) * 2 - 1
-        obs, rew, done, trunc = b.step(act)
-        idx, tobs, ret, ln = b.fetch_done()
-        for k, v in (("obs", obs), ("rew", rew), ("done", done), ("trunc", trunc), ("terms", b.terms)):
-            res["t%d_%s" % (t, k)] = v.cpu().numpy()
-        for k, v in (("idx", idx), ("tobs", tobs), ("ret", ret), ("len", ln)):
-            res["t%d_fetch_%s" % (t, k)] = np.asarray(v)
-    st64, v0, cw = b.get_state64()
-    res.update(state64=st64.cpu().numpy(), v0=v0.cpu().numpy(), cw=cw.cpu().numpy(),
-               state32=b.get_state()[0].cpu().numpy())
-    b.close()
-    return res
-
-
-@pytest.mark.parametrize("cap,n", [(0, 70001), (1, 20003), (2, 20003)])
-def test_straggler_pass_is_bitwise_one_pass(monkeypatch, cap, n):
-    """The straggler deferral (pass 1 stops an env after `cap` accepted steps or at a ground event and
-    spills its loop state; pass 2 resumes it) is bitwise the one-pass lean kernel: rows with ground
-    events, 30 auto-reset steps, done list and terminal rows. cap 0 defers every env (pass 2 then
-    loops over more list slots than its grid holds at N = 70 001)."""
-    ref = _defer_outputs(monkeypatch, -1, n, 30)
-    out = _defer_outputs(monkeypatch, cap, n, 30)
-    assert ref["rows_event"].sum() > 100
-    assert sum(int(v.sum()) for k, v in ref.items() if k.endswith("_done")) > 1000
-    differ = [k for k in ref if not np.array_equal(out[k], ref[k], equal_nan=np.asarray(ref[k]).dtype.kind == "f")]
-    assert not differ, differ
