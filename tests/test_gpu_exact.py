@@ -253,3 +253,21 @@ def test_exact_negative_attitude_limits(oracle_mod, lean):
     assert np.array_equal(out["terms"][:, 3] != 0, ref["terms"][:, 3] != 0)
     assert np.array_equal(out["terms"][:, 4] != 0, ref["terms"][:, 4] != 0)
 
+
+
+@pytest.mark.parametrize("model", [6, 3])
+@pytest.mark.parametrize("n", [1, 63, 65, 257])
+def test_exact_small_and_ragged_batches(model, n, golden6, golden3, lean):
+    """Exact-mode batches that fill no wave or leave a ragged last wave / workgroup: each row is
+    bitwise the same row stepped in the full golden batch (a row does not depend on which envs share
+    its wave, including the padding lanes of the last wave) and within the exact mode's bar."""
+    g = golden6 if model == 6 else golden3
+    full_n = len(g["action"])
+    rows_all = {k: v for k, v in g.items() if getattr(v, "ndim", 0) >= 1 and len(v) == full_n}
+    sel = np.linspace(0, full_n - 1, n).astype(np.int64)
+    rows = {k: v[sel] for k, v in rows_all.items()}
+    out = run_exact(6 if model == 6 else 3, rows, **_kw(model))
+    full = run_exact(6 if model == 6 else 3, rows_all, **_kw(model))
+    for k in ("state_out", "state32", "obs", "reward", "terms", "done", "bounds_violation", "event"):
+        assert np.array_equal(out[k], full[k][sel], equal_nan=out[k].dtype.kind == "f"), k
+    assert floored_rel(out["state_out"], rows["state_out"], g["normalizer"]).max() < STATE_TOL

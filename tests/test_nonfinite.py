@@ -161,15 +161,12 @@ def test_fast_kernel_without_auto_reset_keeps_reporting_done(model):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model", [6, 3])
-@pytest.mark.parametrize("lean", [False, True])
+@pytest.mark.parametrize("model,lean", [(6, False), (3, False), (6, True)])
 def test_exact_mode_stops_like_the_oracle(model, lean, oracle_mod, monkeypatch):
     """DOPRI5 exact mode terminates on non-finite rows (status -1, done) with the oracle's
     state; the other rows bitwise as in a clean batch. lean: the 6DOF lean two-waves-per-SIMD
-    kernel (RR_EXACT_LEAN_MIN_N=0; what N above CUs x 256 runs)."""
+    kernel (RR_EXACT_LEAN_MIN_N=0; what N above CUs x 256 runs; 3DOF has no lean kernel)."""
     if lean:
-        if model == 3:
-            pytest.skip("the lean exact kernel is 6DOF only")
         monkeypatch.setenv("RR_EXACT_LEAN_MIN_N", "0")
     n = 128
     s, a = _clean(model, n, seed=11)
