@@ -421,7 +421,8 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
         gupd, _ = timed(lambda: gt.update(n_epochs=3))
         update["graphed_epoch_ms"] = gupd * 1e3 / 3
         del gt
-        # the loss + backward from rr_ppo_grad (fp32-MFMA HIP pipeline) instead of autograd
+        # the loss + backward + clip + Adam from rr_ppo_update (fp32-MFMA HIP pipeline, chained
+        # minibatches: three launches each) instead of autograd
         gu = GraphedPPOUpdate(pol, opt, ro, batch_size=n, group=grp, fused=True)
         gu.update(n_epochs=1)
         gupd, stats = timed(lambda: gu.update(n_epochs=10))
@@ -444,8 +445,8 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
         train = {"value": iters * args.rollout_steps * n * world / tt, "unit": "env-steps/s",
                  "ms_per_iteration": tt / iters * 1e3,
                  "what": "one training iteration = one collect (n_steps x N env-steps, one hipGraph) + 10 PPO epochs "
-                         "of graphed minibatch updates (SB3 1.6 defaults: n_epochs 10), batch_size N, loss + "
-                         "backward by rr_ppo_grad"}
+                         "of graphed minibatch updates (SB3 1.6 defaults: n_epochs 10), batch_size N, the whole "
+                         "minibatch step (loss + backward + clip + Adam) by rr_ppo_update, chained"}
     env.close()
     # roofline of the collect kernel (rollout_step_kernel<..., MULTI = true>): the policy towers
     # are the contraction (fp32 MFMA in the default precision), so the bound is the MFMA peak;

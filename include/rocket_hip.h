@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 11
+#define RR_ABI_VERSION 12
 
 /* error codes */
 #define RR_OK 0
@@ -386,6 +386,30 @@ int rr_clip_adam(int n_tensors, float* const* params, float* const* grads, float
                  float* const* exp_avg_sq, float* const* step, const int64_t* numel, float max_grad_norm,
                  const float* lr, double beta1, double beta2, float eps, void* workspace, int64_t workspace_bytes,
                  void* stream);
+
+/* One whole PPO minibatch step: rr_ppo_grad followed by rr_clip_adam over the same 13 tensors
+ * (rr_ppo_grad's order; exp_avg / exp_avg_sq / step as rr_clip_adam's), replacing SB3 1.6
+ * PPO.train's loss.backward(), clip_grad_norm_ and optimizer.step() for one minibatch
+ * (main_6DOF.py:62-69) without a multi-GPU all_reduce between them. It takes three launches
+ * where the two calls take five:
+ *   - the gradient finish also sums the squared gradients for the clip;
+ *   - the optimizer step also refreshes the packed tower images of the gradient launch;
+ *   - with next_idx (next_batch rows, 2 <= next_batch <= batch) the optimizer launch also sums
+ *     the NEXT minibatch's advantage statistics.
+ * A call with flags & RR_PPO_CHAINED skips the packing / statistics launch and uses what the
+ * previous rr_ppo_update on the same workspace left there. That previous call must have been
+ * given next_idx = this idx, next_batch = this batch, and nothing else may have written the
+ * parameters since. Without the flag the call packs from the parameters itself (four launches).
+ * Arithmetic as the two calls, except that the clip's norm sums the squares in the finish's
+ * order. workspace: device, 16-B aligned, rr_ppo_update_workspace_size bytes; lr a device float. */
+#define RR_PPO_CHAINED 0x1u
+int rr_ppo_update_workspace_size(int obs_dim, int act_dim, int64_t batch, int64_t* bytes);
+int rr_ppo_update(int obs_dim, int act_dim, float* const* params, float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, float* const* step, const float* obs, const float* actions,
+                  const float* old_log_prob, const float* advantages, const float* returns, const int64_t* idx,
+                  int64_t batch, const int64_t* next_idx, int64_t next_batch, float clip_range, float ent_coef,
+                  float vf_coef, float max_grad_norm, const float* lr, double beta1, double beta2, float eps,
+                  float* stats, uint32_t flags, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

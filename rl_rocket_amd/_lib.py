@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(HERE, "librocket_hip.so")  # override: diagnostics only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rocket_hip.h")
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_ENOMEM = 0, -1, -2, -3
 RR_MODEL_3DOF, RR_MODEL_6DOF = 3, 6
@@ -128,6 +128,11 @@ SIGNATURES = {
     "rr_ppo_workspace_size": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int64, _P]),
     "rr_ppo_grad": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_int64,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, ctypes.c_int64, _P]),
+    "rr_ppo_update_workspace_size": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int64, _P]),
+    "rr_ppo_update": (ctypes.c_int, [ctypes.c_int, ctypes.c_int] + [_P] * 11 + [ctypes.c_int64, _P, ctypes.c_int64,
+                                     ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_float, _P, ctypes.c_uint32, _P,
+                                     ctypes.c_int64, _P]),
 }
 
 _LIB = None

@@ -2650,12 +2650,91 @@ int rr_ppo_grad(int obs_dim, int act_dim, const float* const* params, float* con
         hipLaunchKernelGGL((ppo_grad_kernel<O, A>), dim3(nwg, 2), dim3(ppo::kThreads), 0, s, obs, actions,
                            old_log_prob, advantages, returns, idx, batch, clip_range, vf_coef, adv_part, pack, part);
         hipLaunchKernelGGL((ppo_finish_kernel<O, A>), dim3((PT::SIZE + kFinElems - 1) / kFinElems, 2), dim3(256), 0, s, part, nwg, batch,
-                           ent_coef, ps, pg, stats);
+                           ent_coef, ps, pg, stats, nullptr, nullptr);
     };
     if (obs_dim == 14) run(std::integral_constant<int, 14>{}, std::integral_constant<int, 3>{});
     else run(std::integral_constant<int, 7>{}, std::integral_constant<int, 2>{});
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_ppo_grad: launch");
+}
+
+int rr_ppo_update_workspace_size(int obs_dim, int act_dim, int64_t batch, int64_t* bytes)
+{
+    int64_t ppo = 0;
+    const int rc = rr_ppo_workspace_size(obs_dim, act_dim, batch, &ppo);
+    if (rc != RR_OK) return rc;
+    // + the finish kernel's squared-gradient sums (two towers) and the step count, 16-B rows
+    const int64_t fin = (ppo_part_floats(obs_dim, act_dim) + kFinElems - 1) / kFinElems;
+    *bytes = (ppo + 15) / 16 * 16 + (2 * fin + 1 + 3) / 4 * 16;
+    return RR_OK;
+}
+
+int rr_ppo_update(int obs_dim, int act_dim, float* const* params, float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, float* const* step, const float* obs, const float* actions,
+                  const float* old_log_prob, const float* advantages, const float* returns, const int64_t* idx,
+                  int64_t batch, const int64_t* next_idx, int64_t next_batch, float clip_range, float ent_coef,
+                  float vf_coef, float max_grad_norm, const float* lr, double beta1, double beta2, float eps,
+                  float* stats, uint32_t flags, void* workspace, int64_t workspace_bytes, void* stream)
+{
+    int64_t need = 0, ppo_bytes = 0;
+    int rc = rr_ppo_update_workspace_size(obs_dim, act_dim, batch, &need);
+    if (rc != RR_OK) return rc;
+    rr_ppo_workspace_size(obs_dim, act_dim, batch, &ppo_bytes);
+    if (!params || !grads || !exp_avg || !exp_avg_sq || !step || !obs || !actions || !old_log_prob || !advantages ||
+        !returns || !idx || !lr || !workspace)
+        return fail(RR_EINVAL, "rr_ppo_update: null argument");
+    if (workspace_bytes < need) return fail(RR_EINVAL, "rr_ppo_update: workspace smaller than rr_ppo_update_workspace_size");
+    if (((uintptr_t)workspace & 15) != 0) return fail(RR_EINVAL, "rr_ppo_update: workspace must be 16-B aligned");
+    if (!(clip_range >= 0.0f)) return fail(RR_EINVAL, "rr_ppo_update: clip_range must be >= 0");
+    if (flags & ~(uint32_t)RR_PPO_CHAINED) return fail(RR_EINVAL, "rr_ppo_update: unknown flag bits");
+    if (next_idx && !(next_batch >= 2 && next_batch <= batch))
+        return fail(RR_EINVAL, "rr_ppo_update: next_batch must be in [2, batch]");
+    const int na = act_dim, no = obs_dim;
+    const int64_t numel[13] = {64 * no, 64, 64 * 64, 64, 64 * no, 64, 64 * 64, 64, 64 * na, na, 64, 1, na};
+    PolSrc ps;
+    PolGrad pg;
+    AdamList a = {};
+    a.n = 13;
+    for (int k = 0; k < 13; ++k) {
+        if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || !step[k])
+            return fail(RR_EINVAL, "rr_ppo_update: null parameter, gradient or optimizer-state tensor");
+        ps.p[k] = params[k];
+        pg.p[k] = grads[k];
+        a.param[k] = params[k];
+        a.grad[k] = grads[k];
+        a.exp_avg[k] = exp_avg[k];
+        a.exp_avg_sq[k] = exp_avg_sq[k];
+        a.step[k] = step[k];
+        a.start[k + 1] = a.start[k] + numel[k];
+    }
+    hipStream_t s = (hipStream_t)stream;
+    double* adv_part = (double*)workspace;
+    float* part = (float*)((char*)workspace + 2 * ppo::kAdvPart * sizeof(double));
+    float* normw = (float*)((char*)workspace + (ppo_bytes + 15) / 16 * 16);
+    const int nwg = (int)ppo_nwg(batch);
+    const int nbp = (int)((a.start[13] + kAdamThreads - 1) / kAdamThreads);
+    const AdvNext nx = {advantages, next_idx, next_idx ? next_batch : 0, adv_part};
+    auto run = [&](auto obs_c, auto act_c) {
+        constexpr int O = decltype(obs_c)::value, A = decltype(act_c)::value;
+        using PT = ppo::Part<O, A>;
+        using K = ppo::Pack<O, A>;
+        constexpr int nfin = (PT::SIZE + kFinElems - 1) / kFinElems;
+        float* pack = part + 2 * (int64_t)nwg * PT::SIZE;
+        if (!(flags & RR_PPO_CHAINED))
+            hipLaunchKernelGGL((ppo_prep_kernel<O, A>), dim3(ppo::kAdvPart + (2 * K::SIZE + 255) / 256), dim3(256), 0, s,
+                               advantages, idx, batch, adv_part, ps, pack);
+        hipLaunchKernelGGL((ppo_grad_kernel<O, A>), dim3(nwg, 2), dim3(ppo::kThreads), 0, s, obs, actions,
+                           old_log_prob, advantages, returns, idx, batch, clip_range, vf_coef, adv_part, pack, part);
+        hipLaunchKernelGGL((ppo_finish_kernel<O, A>), dim3(nfin, 2), dim3(256), 0, s, part, nwg, batch, ent_coef, ps, pg,
+                           stats, normw, (const float*)step[0]);
+        hipLaunchKernelGGL((adam_chain_kernel<O, A>), dim3(nbp + (next_idx ? ppo::kAdvPart / 4 : 0)), dim3(kAdamThreads),
+                           0, s, a, (const float*)normw, 2 * nfin, max_grad_norm, lr, (float)beta1, (float)beta2,
+                           (float)(1.0 - beta1), (float)(1.0 - beta2), eps, pack, nx, nbp);
+    };
+    if (obs_dim == 14) run(std::integral_constant<int, 14>{}, std::integral_constant<int, 3>{});
+    else run(std::integral_constant<int, 7>{}, std::integral_constant<int, 2>{});
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? RR_OK : hip_fail(err, "rr_ppo_update: launch");
 }
 
 

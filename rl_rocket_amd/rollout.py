@@ -622,6 +622,87 @@ class ClipAdam:
                    "rr_clip_adam")
 
 
+class PPOUpdate(PPOGrad):
+    """A whole PPO minibatch step — ``PPOGrad`` then ``ClipAdam``'s clip + Adam step on the same 13
+    tensors — as ONE library call (``rr_ppo_update``). Without a gradient all_reduce between the
+    two halves, the clip's norm is summed by the gradient finish. The optimizer launch also repacks
+    the towers for the next call and sums the next minibatch's advantage statistics. A chain of
+    minibatches therefore takes three launches each instead of five; the first takes four.
+
+    ``__call__(idx, next_idx=None, chained=False)``:
+      * ``chained=True`` says that the previous call on this object was given ``next_idx=idx`` and
+        that nothing else has written the parameters since.
+      * The optimizer is the source of truth, as with ``ClipAdam``: its exp_avg / exp_avg_sq /
+        step tensors are updated in place.
+      * ``lr`` is read from a device scalar. ``sync_lr()`` refreshes it, and eager calls do so
+        themselves."""
+
+    def __init__(self, policy, optimizer, ro, batch_size, clip_range=0.2, ent_coef=0.01, vf_coef=0.5,
+                 max_grad_norm=0.5):
+        import ctypes
+
+        from . import _lib
+
+        super().__init__(policy, ro, batch_size, clip_range, ent_coef, vf_coef)
+        if not clip_adam_supported(optimizer, list(policy.parameters())):
+            raise ValueError("PPOUpdate needs a capturable torch.optim.Adam over the policy's parameters "
+                             "(one group, no weight decay / amsgrad / maximize)")
+        self.opt, self.max_norm = optimizer, float(max_grad_norm) if max_grad_norm is not None else 0.0
+        dev = self.ws.device
+        for p in self.params:
+            st = optimizer.state[p]
+            if not st:
+                st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            if not st["step"].is_cuda or st["step"].dtype != torch.float32:
+                raise ValueError("PPOUpdate needs the capturable Adam's device float32 step tensors")
+        self._state = [(optimizer.state[p]["exp_avg"], optimizer.state[p]["exp_avg_sq"], optimizer.state[p]["step"])
+                       for p in self.params]
+        P = ctypes.c_void_p * 13
+        self._params_w = P(*[p.data_ptr() for p in self.params])
+        self._m, self._v, self._s = (P(*[st[k].data_ptr() for st in self._state]) for k in range(3))
+        self.lr = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.sync_lr()
+        nbytes = ctypes.c_int64()
+        _lib.check(self._lib.rr_ppo_update_workspace_size(self.ns, self.na, self.bs, ctypes.byref(nbytes)),
+                   "rr_ppo_update_workspace_size")
+        self.ws = torch.empty((nbytes.value + 15) // 16 * 4, dtype=torch.float32, device=dev)
+        self._nbytes = nbytes.value
+
+    def sync_lr(self):
+        self.lr.fill_(float(self.opt.param_groups[0]["lr"]))
+
+    def __call__(self, idx, next_idx=None, chained=False):
+        from . import _lib
+
+        c = self._c
+        for t in (idx,) if next_idx is None else (idx, next_idx):
+            if (t.dtype != torch.int64 or not 2 <= t.numel() <= self.bs or not t.is_contiguous()
+                    or t.device != self.ws.device):
+                raise ValueError("idx / next_idx must be contiguous int64 device tensors of 2 .. batch_size rows")
+        if next_idx is not None and next_idx.numel() > idx.numel():
+            raise ValueError("next_idx may not be longer than idx")
+        for p, g, (m, v, s) in zip(self.params, self._grads, self._state):
+            st = self.opt.state[p]
+            if p.grad is not g or st["exp_avg"] is not m or st["exp_avg_sq"] is not v or st["step"] is not s:
+                raise RuntimeError("a gradient or Adam state tensor was replaced; PPOUpdate holds their addresses")
+        if not torch.cuda.is_current_stream_capturing():
+            self.sync_lr()
+        grp = self.opt.param_groups[0]
+        b1, b2 = grp["betas"]
+        clip, ent, vf = self.coef
+        o, a, lp, adv, ret = self.data
+        nxt = None if next_idx is None else next_idx.data_ptr()
+        _lib.check(self._lib.rr_ppo_update(
+            self.ns, self.na, self._params_w, self._dst, self._m, self._v, self._s, o.data_ptr(), a.data_ptr(),
+            lp.data_ptr(), adv.data_ptr(), ret.data_ptr(), idx.data_ptr(), idx.numel(), nxt,
+            0 if next_idx is None else next_idx.numel(), clip, ent, vf, self.max_norm, self.lr.data_ptr(), float(b1),
+            float(b2), float(grp["eps"]), self.stats.data_ptr(), 1 if chained else 0, self.ws.data_ptr(),
+            self._nbytes, c.c_void_p(torch.cuda.current_stream(self.ws.device).cuda_stream)), "rr_ppo_update")
+        return self.stats
+
+
 def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=0.2, ent_coef=0.01,
                vf_coef=0.5, max_grad_norm=0.5, generator=None, group=None, fused=False):
     """SB3 1.6 PPO.train on the device-resident rollout (advantage normalisation per
@@ -645,10 +726,19 @@ def ppo_update(policy, optimizer, ro, n_epochs=10, batch_size=65536, clip_range=
             # refuses it) and failing there would leave the epoch's earlier Adam steps applied
             raise ValueError("n_steps * num_envs = %d leaves a 1-row last minibatch at batch_size %d (rr_ppo_grad "
                              "needs >= 2 rows); choose another batch_size" % (n, batch_size))
-        grad = PPOGrad(policy, ro, min(batch_size, n), clip_range, ent_coef, vf_coef)
         params = list(policy.parameters())
-        adam = ClipAdam(optimizer, params, max_grad_norm) if clip_adam_supported(optimizer, params) else None
         stats = None
+        if group is None and clip_adam_supported(optimizer, params):
+            # the whole minibatch step in one call, chained: each call sums the next one's statistics
+            step = PPOUpdate(policy, optimizer, ro, min(batch_size, n), clip_range, ent_coef, vf_coef, max_grad_norm)
+            for _ in range(n_epochs):
+                perm = torch.randperm(n, device=ro.obs.device, generator=generator)
+                for s in range(0, n, step.bs):
+                    nxt = perm[s + step.bs:s + 2 * step.bs] if s + step.bs < n else None
+                    stats = step(perm[s:s + step.bs], nxt, chained=s > 0)
+            return {} if stats is None else dict(zip(("policy_loss", "value_loss", "entropy"), stats[:3].tolist()))
+        grad = PPOGrad(policy, ro, min(batch_size, n), clip_range, ent_coef, vf_coef)
+        adam = ClipAdam(optimizer, params, max_grad_norm) if clip_adam_supported(optimizer, params) else None
         for _ in range(n_epochs):
             perm = torch.randperm(n, device=ro.obs.device, generator=generator)
             for s in range(0, n, grad.bs):
@@ -749,19 +839,23 @@ class GraphedPPOUpdate:
         if fused is None:
             fused = fused_grad_supported(policy, ro.env.state_dim, ro.env.action_dim)
         self.fused = bool(fused)
-        self._grad = PPOGrad(policy, ro, batch_size, clip_range, ent_coef, vf_coef) if self.fused else None
+        # fused, one replica, capturable Adam: the chained whole-minibatch call (rr_ppo_update)
+        self._update = (PPOUpdate(policy, optimizer, ro, batch_size, clip_range, ent_coef, vf_coef, max_grad_norm)
+                        if self.fused and group is None and clip_adam_supported(optimizer, params) else None)
+        self._grad = (PPOGrad(policy, ro, batch_size, clip_range, ent_coef, vf_coef)
+                      if self.fused and self._update is None else None)
         self._adam = (ClipAdam(optimizer, params, max_grad_norm)
-                      if self.fused and clip_adam_supported(optimizer, params) else None)
+                      if self._grad is not None and clip_adam_supported(optimizer, params) else None)
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for k in range(3):
-                self._step(self._mb(k % self.n_mb))
+                self._step(self._mb(k % self.n_mb), k % self.n_mb)
         torch.cuda.current_stream(dev).wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             for k in range(self.n_mb):
-                self.stats = self._step(self._mb(k))
+                self.stats = self._step(self._mb(k), k)
         with torch.no_grad():
             for p, v in zip(params, saved_p):
                 p.copy_(v)
@@ -781,9 +875,12 @@ class GraphedPPOUpdate:
     def _mb(self, k):
         return self.perm[k * self.bs:(k + 1) * self.bs]
 
-    def _step(self, i):
+    def _step(self, i, k=0):
         clip_range, ent_coef, vf_coef, max_grad_norm = self.coef
         pol = self.policy
+        if self._update is not None:
+            st = self._update(i, self._mb(k + 1) if k + 1 < self.n_mb else None, chained=k > 0)
+            return {"policy_loss": st[0], "value_loss": st[1], "entropy": st[2]}
         if self.fused:
             st = self._grad(i)
             if self.group is not None:
@@ -814,8 +911,9 @@ class GraphedPPOUpdate:
     def update(self, n_epochs=10, generator=None):
         """n_epochs passes over the rollout in shuffled minibatches (ppo_update's order:
         one torch.randperm per epoch)."""
-        if self._adam is not None:
-            self._adam.sync_lr()  # the graph reads lr from the device: follow param_groups[0]["lr"]
+        for o in (self._adam, self._update):
+            if o is not None:
+                o.sync_lr()  # the graph reads lr from the device: follow param_groups[0]["lr"]
         for _ in range(n_epochs):
             self.perm.copy_(torch.randperm(self.n, device=self.obs.device, generator=generator))
             self.graph.replay()

@@ -306,3 +306,43 @@ def test_rollout_and_learner_forwards_agree():
     assert abs(approx_kl) <= 1e-9
     assert vl ** 0.5 <= 1e-5 * (1.0 + rms_v)
     env.close()
+
+
+def test_ppo_update_chain_carries_what_a_fresh_prep_computes():
+    """rr_ppo_update chained (each call's optimizer launch repacks the towers from the updated
+    parameters — the inverse of the pack — and sums the next minibatch's advantage statistics)
+    against the same calls each packing and summing for itself: after 2 epochs x 4 minibatches
+    (the last one 2 rows short, a shorter next_batch) every parameter, gradient and Adam state
+    tensor is bitwise equal. Both paths also stay within fp32 rounding of PPOGrad + ClipAdam (the
+    clip's norm is summed in another order)."""
+    import torch
+    from rl_rocket_amd.rollout import ClipAdam, PPOGrad, PPOUpdate
+
+    env, pol, ro = _rollout_for_update()
+    n = ro.n_steps * ro.env.num_envs
+    bs = 16384
+    pols = [copy.deepcopy(pol) for _ in range(3)]
+    opts = [torch.optim.Adam(p.parameters(), lr=1e-3, eps=1.0, capturable=True) for p in pols]
+    upd = [PPOUpdate(pols[k], opts[k], ro, bs) for k in range(2)]
+    grad, adam = PPOGrad(pols[2], ro, bs), ClipAdam(opts[2], list(pols[2].parameters()), 0.5)
+    g = torch.Generator("cuda:0").manual_seed(5)
+    for _ in range(2):
+        perm = torch.randperm(n, device="cuda:0", generator=g)[:4 * bs - 2]
+        mbs = [perm[s:s + bs] for s in range(0, len(perm), bs)]
+        for k, idx in enumerate(mbs):
+            nxt = mbs[k + 1] if k + 1 < len(mbs) else None
+            upd[0](idx, nxt, chained=k > 0)
+            upd[1](idx)
+            grad(idx)
+            adam()
+    torch.cuda.synchronize()
+    for x, y, z in zip(*[list(p.parameters()) for p in pols]):
+        assert torch.equal(x, y)
+        assert torch.equal(x.grad, y.grad)
+        assert torch.equal(opts[0].state[x]["exp_avg"], opts[1].state[y]["exp_avg"])
+        assert torch.equal(opts[0].state[x]["exp_avg_sq"], opts[1].state[y]["exp_avg_sq"])
+        assert float(opts[0].state[x]["step"]) == float(opts[2].state[z]["step"]) == 8
+        assert (x - z).abs().max().item() <= 1e-6 * max(1.0, z.abs().max().item())
+    with pytest.raises(ValueError):
+        upd[0](mbs[0][:bs - 2], mbs[1])  # next_idx longer than idx
+    env.close()
