@@ -669,6 +669,7 @@ class PPOUpdate(PPOGrad):
                    "rr_ppo_update_workspace_size")
         self.ws = torch.empty((nbytes.value + 15) // 16 * 4, dtype=torch.float32, device=dev)
         self._nbytes = nbytes.value
+        self._next = None  # (address, rows) of the last call's next_idx: what chained=True may follow
 
     def sync_lr(self):
         self.lr.fill_(float(self.opt.param_groups[0]["lr"]))
@@ -683,6 +684,8 @@ class PPOUpdate(PPOGrad):
                 raise ValueError("idx / next_idx must be contiguous int64 device tensors of 2 .. batch_size rows")
         if next_idx is not None and next_idx.numel() > idx.numel():
             raise ValueError("next_idx may not be longer than idx")
+        if chained and self._next != (idx.data_ptr(), idx.numel()):
+            raise ValueError("chained=True needs the previous call on this PPOUpdate to have had next_idx=idx")
         for p, g, (m, v, s) in zip(self.params, self._grads, self._state):
             st = self.opt.state[p]
             if p.grad is not g or st["exp_avg"] is not m or st["exp_avg_sq"] is not v or st["step"] is not s:
@@ -700,6 +703,7 @@ class PPOUpdate(PPOGrad):
             0 if next_idx is None else next_idx.numel(), clip, ent, vf, self.max_norm, self.lr.data_ptr(), float(b1),
             float(b2), float(grp["eps"]), self.stats.data_ptr(), 1 if chained else 0, self.ws.data_ptr(),
             self._nbytes, c.c_void_p(torch.cuda.current_stream(self.ws.device).cuda_stream)), "rr_ppo_update")
+        self._next = None if next_idx is None else (next_idx.data_ptr(), next_idx.numel())
         return self.stats
 
 

@@ -345,4 +345,6 @@ def test_ppo_update_chain_carries_what_a_fresh_prep_computes():
         assert (x - z).abs().max().item() <= 1e-6 * max(1.0, z.abs().max().item())
     with pytest.raises(ValueError):
         upd[0](mbs[0][:bs - 2], mbs[1])  # next_idx longer than idx
+    with pytest.raises(ValueError):
+        upd[0](mbs[1], chained=True)  # the last call handed over no next minibatch
     env.close()
