@@ -2661,8 +2661,10 @@ int rr_ppo_grad(int obs_dim, int act_dim, const float* const* params, float* con
 int rr_ppo_update_workspace_size(int obs_dim, int act_dim, int64_t batch, int64_t* bytes)
 {
     int64_t ppo = 0;
-    const int rc = rr_ppo_workspace_size(obs_dim, act_dim, batch, &ppo);
-    if (rc != RR_OK) return rc;
+    if (!ppo_part_floats(obs_dim, act_dim))
+        return fail(RR_EINVAL, "rr_ppo_update_workspace_size: supported (obs_dim, act_dim) are (14, 3) and (7, 2)");
+    if (batch < 2 || !bytes) return fail(RR_EINVAL, "rr_ppo_update_workspace_size: batch >= 2 and bytes required");
+    rr_ppo_workspace_size(obs_dim, act_dim, batch, &ppo);
     // + the finish kernel's squared-gradient sums (two towers) and the step count, 16-B rows
     const int64_t fin = (ppo_part_floats(obs_dim, act_dim) + kFinElems - 1) / kFinElems;
     *bytes = (ppo + 15) / 16 * 16 + (2 * fin + 1 + 3) / 4 * 16;

@@ -106,10 +106,10 @@ def _ptrs(k, null_at=None):
     return arr
 
 
-def test_abi_8_to_11_entry_points_refuse_bad_arguments_before_any_hip_call():
-    """Every entry point added in ABI 8-11 (rr_gather_rows, rr_copy_terminal, rr_step_rows,
-    rr_host_alloc / rr_host_free, rr_ppo_grad, rr_clip_adam, their workspace sizes, the rr_policy_*
-    and rollout calls) returns RR_EINVAL with a message naming itself for null handles, null or
+def test_abi_8_to_12_entry_points_refuse_bad_arguments_before_any_hip_call():
+    """Every entry point added in ABI 8-12 (rr_gather_rows, rr_copy_terminal, rr_step_rows,
+    rr_host_alloc / rr_host_free, rr_ppo_grad, rr_clip_adam, rr_ppo_update, their workspace sizes,
+    the rr_policy_* and rollout calls) returns RR_EINVAL with a message naming itself for null handles, null or
     inconsistent arguments and bad sizes — without touching HIP (this host has no GPU; tools/
     sanitize.sh runs this test under ASan + UBSan). Valid host-only calls (layout / workspace
     sizes) return the documented values."""
@@ -198,6 +198,29 @@ def test_abi_8_to_11_entry_points_refuse_bad_arguments_before_any_hip_call():
     refused(adam(13, _ptrs(13), numel, 1 << 20), "rr_clip_adam")  # empty tensor
     numel[12] = 64
     refused(adam(13, _ptrs(13), numel, 8), "rr_clip_adam")  # workspace too small
+    # ABI 12: the chained minibatch step (rr_ppo_grad + rr_clip_adam in one call)
+    assert lib.rr_ppo_update_workspace_size(14, 3, 65536, ctypes.byref(ws)) == 0 and ws.value > small
+    refused(lib.rr_ppo_update_workspace_size(14, 3, 1, ctypes.byref(ws)), "rr_ppo_update_workspace_size")
+    refused(lib.rr_ppo_update_workspace_size(9, 3, 64, ctypes.byref(ws)), "rr_ppo_update_workspace_size")
+
+    def update(params=None, state_null=None, batch=64, nxt=None, next_batch=0, clip=0.2, flags=0, wsp=fake,
+               ws_bytes=1 << 30):
+        lists = [_ptrs(13, null_at=12) if state_null == k else _ptrs(13) for k in range(4)]
+        return lib.rr_ppo_update(14, 3, _ptrs(13) if params is None else params, *lists, *args, batch, nxt,
+                                 next_batch, ctypes.c_float(clip), ctypes.c_float(0.01), ctypes.c_float(0.5),
+                                 ctypes.c_float(0.5), lr, ctypes.c_double(0.9), ctypes.c_double(0.999),
+                                 ctypes.c_float(1e-5), None, flags, wsp, ws_bytes, None)
+
+    refused(update(params=_ptrs(13, null_at=3)), "rr_ppo_update")
+    for k in range(4):  # grads, exp_avg, exp_avg_sq, step
+        refused(update(state_null=k), "rr_ppo_update")
+    refused(update(batch=1), "rr_ppo_update")
+    refused(update(ws_bytes=16), "rr_ppo_update")  # workspace too small
+    refused(update(wsp=V(0x10008)), "rr_ppo_update")  # misaligned
+    refused(update(clip=-1.0), "rr_ppo_update")
+    refused(update(flags=0x2), "rr_ppo_update")  # unknown flag
+    refused(update(nxt=fake, next_batch=1), "rr_ppo_update")
+    refused(update(nxt=fake, next_batch=65), "rr_ppo_update")  # longer than this minibatch
     # rollouts / GAE (kept from ABI 3-7)
     refused(lib.rr_gae(16, 0, fake, fake, fake, fake, fake, ctypes.c_float(0.99), ctypes.c_float(0.95), fake, fake,
                        None), "rr_gae")
