@@ -15,8 +15,9 @@ SRC = os.path.join(HERE, "csrc", "rocket_hip.hip")
 # 33 VGPRs to scratch at one wave per SIMD (r03e), with it none
 SRC_EXACT = os.path.join(HERE, "csrc", "rocket_exact.hip")
 EXACT_FLAGS = ["-mllvm", "-amdgpu-schedule-metric-bias=100"]
-# the rollout collect kernels' translation unit (rocket_hip.hip under RR_TU_COLLECT), with the MFMA
-# accumulators in VGPRs: no v_accvgpr_read per tanh input (5.5 % faster collect, round 4)
+# the rollout collect and PPO learner kernels' translation unit (rocket_hip.hip under RR_TU_COLLECT),
+# with the MFMA accumulators in VGPRs: no v_accvgpr_read per tanh input (5.5 % faster collect,
+# round 4; the learner's minibatch 3 % faster, round 6)
 SRC_COLLECT = os.path.join(HERE, "csrc", "rocket_collect.hip")
 COLLECT_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("rocket_dopri5.inc", "rocket_policy.inc", "rocket_rollout.inc", "rocket_ppo.inc",

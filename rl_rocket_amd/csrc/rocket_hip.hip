@@ -1341,10 +1341,9 @@ __global__ __launch_bounds__(kBlock) void copy_done_rows_kernel(const uint64_t* 
 // On-device PPO rollout kernels (fused MlpPolicy forward on fp32 MFMA, bootstrap, GAE)
 #include "rocket_policy.inc"
 #include "rocket_rollout.inc"
-#ifndef RR_TU_COLLECT
-// PPO minibatch gradient (loss + backward of the MlpPolicy on fp32 MFMA)
+// PPO learner (loss + backward of the MlpPolicy on fp32 MFMA, clip + Adam): its types in both
+// translation units, its kernels launched from the collect TU (rrc_launch_learner)
 #include "rocket_ppo.inc"
-#endif  // RR_TU_COLLECT
 #endif  // RR_TU_EXACT
 
 // Exact-integrator mode (RR_INT_DOPRI5): fp64 scipy RK45 restatement, compiled without
@@ -1427,6 +1426,50 @@ extern "C" __attribute__((visibility("hidden"))) int rrc_launch_collect(int mode
 #undef RR_COLLECT
     return (int)hipGetLastError();
 }
+
+// the learner's launches (hidden: not part of the C-ABI), for rr_ppo_grad / rr_ppo_update /
+// rr_clip_adam, which validated the arguments and carved the workspace into `launch` (a PpoLaunch of
+// the calling TU). Compiled here with the MFMA accumulators in VGPRs: the gradient kernel's loop
+// then moves ~740 fewer registers between AGPRs and VGPRs per launch, bitwise the same gradients
+// (profiles/r06/ppo_vf/)
+extern "C" __attribute__((visibility("hidden"))) int rrc_launch_learner(const void* launch, void* stream)
+{
+    PpoLaunch L;
+    std::memcpy(&L, launch, sizeof(PpoLaunch));
+    hipStream_t s = (hipStream_t)stream;
+    if (L.op == 2) {
+        const dim3 grid((unsigned)((L.a.start[L.a.n] + kAdamThreads - 1) / kAdamThreads));
+        hipLaunchKernelGGL(adam_norm_kernel, grid, dim3(kAdamThreads), 0, s, L.a, L.work);
+        hipLaunchKernelGGL(adam_step_kernel, grid, dim3(kAdamThreads), 0, s, L.a, L.work, L.max_norm, L.lr, L.beta1,
+                           L.beta2, L.w1, L.w2, L.eps);
+        return (int)hipGetLastError();
+    }
+    const bool update = L.op == 1;
+    auto run = [&](auto obs_c, auto act_c) {
+        constexpr int O = decltype(obs_c)::value, A = decltype(act_c)::value;
+        using PT = ppo::Part<O, A>;
+        using K = ppo::Pack<O, A>;
+        constexpr int nfin = (PT::SIZE + kFinElems - 1) / kFinElems;
+        if (!(update && (L.flags & RR_PPO_CHAINED)))
+            hipLaunchKernelGGL((ppo_prep_kernel<O, A>), dim3(ppo::kAdvPart + (2 * K::SIZE + 255) / 256), dim3(256), 0, s,
+                               L.advantages, L.idx, L.batch, L.adv_part, L.ps, L.pack);
+        hipLaunchKernelGGL((ppo_grad_kernel<O, A>), dim3(L.nwg, 2), dim3(ppo::kThreads), 0, s, L.obs, L.actions,
+                           L.old_log_prob, L.advantages, L.returns, L.idx, L.batch, L.clip, L.vf, L.adv_part, L.pack,
+                           L.part);
+        hipLaunchKernelGGL((ppo_finish_kernel<O, A>), dim3(nfin, 2), dim3(256), 0, s, L.part, L.nwg, L.batch, L.ent,
+                           L.ps, L.pg, L.stats, update ? L.normw : nullptr,
+                           update ? (const float*)L.a.step[0] : nullptr);
+        if (update) {
+            const AdvNext nx = {L.advantages, L.next_idx, L.next_idx ? L.next_batch : 0, L.adv_part};
+            hipLaunchKernelGGL((adam_chain_kernel<O, A>), dim3(L.nbp + (L.next_idx ? ppo::kAdvPart / 4 : 0)),
+                               dim3(kAdamThreads), 0, s, L.a, (const float*)L.normw, 2 * nfin, L.max_norm, L.lr,
+                               L.beta1, L.beta2, L.w1, L.w2, L.eps, L.pack, nx, L.nbp);
+        }
+    };
+    if (L.obs_dim == 14) run(std::integral_constant<int, 14>{}, std::integral_constant<int, 3>{});
+    else run(std::integral_constant<int, 7>{}, std::integral_constant<int, 2>{});
+    return (int)hipGetLastError();
+}
 #else  // the main translation unit: host side
 
 // defined by the exact / collect translation units; these weak stand-ins (a library built from this
@@ -1440,6 +1483,10 @@ extern "C" __attribute__((weak, visibility("hidden"))) int rrx_launch_exact(int,
 extern "C" __attribute__((weak, visibility("hidden"))) int rrc_launch_collect(int, int, int, unsigned, float*,
                                                                             uint32_t, uint32_t, const void*,
                                                                             const void*, const void*, void*)
+{
+    return (int)hipErrorInvalidDeviceFunction;
+}
+extern "C" __attribute__((weak, visibility("hidden"))) int rrc_launch_learner(const void*, void*)
 {
     return (int)hipErrorInvalidDeviceFunction;
 }
@@ -2563,6 +2610,17 @@ int64_t ppo_pack_floats(int obs_dim, int act_dim)
 {
     return obs_dim == 14 ? ppo::Pack<14, 3>::SIZE : ppo::Pack<7, 2>::SIZE;
 }
+
+// rr_ppo_workspace_size's layout: advantage partial sums | 2 towers x nwg partial-gradient vectors |
+// 2 packed tower images (16-B aligned: Part::SIZE % 4 == 0)
+void ppo_carve(PpoLaunch& L, int obs_dim, int act_dim, int64_t batch, void* workspace)
+{
+    L.obs_dim = obs_dim;
+    L.nwg = (int)ppo_nwg(batch);
+    L.adv_part = (double*)workspace;
+    L.part = (float*)((char*)workspace + 2 * ppo::kAdvPart * sizeof(double));
+    L.pack = L.part + 2 * (int64_t)L.nwg * ppo_part_floats(obs_dim, act_dim);
+}
 }  // namespace
 
 int rr_clip_adam_workspace_size(int64_t total_elements, int64_t* bytes)
@@ -2595,13 +2653,18 @@ int rr_clip_adam(int n_tensors, float* const* params, float* const* grads, float
     int64_t need = 0;
     rr_clip_adam_workspace_size(a.start[n_tensors], &need);
     if (workspace_bytes < need) return fail(RR_EINVAL, "rr_clip_adam: workspace smaller than rr_clip_adam_workspace_size");
-    const dim3 grid((unsigned)((a.start[n_tensors] + kAdamThreads - 1) / kAdamThreads));
-    hipStream_t s = (hipStream_t)stream;
-    float* work = (float*)workspace;
-    hipLaunchKernelGGL(adam_norm_kernel, grid, dim3(kAdamThreads), 0, s, a, work);
-    hipLaunchKernelGGL(adam_step_kernel, grid, dim3(kAdamThreads), 0, s, a, work, max_grad_norm, lr, (float)beta1,
-                       (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps);
-    hipError_t err = hipGetLastError();
+    PpoLaunch L = {};
+    L.op = 2;
+    L.a = a;
+    L.work = (float*)workspace;
+    L.max_norm = max_grad_norm;
+    L.lr = lr;
+    L.beta1 = (float)beta1;
+    L.beta2 = (float)beta2;
+    L.w1 = (float)(1.0 - beta1);
+    L.w2 = (float)(1.0 - beta2);
+    L.eps = eps;
+    const hipError_t err = (hipError_t)rrc_launch_learner(&L, stream);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_clip_adam: launch");
 }
 
@@ -2629,32 +2692,26 @@ int rr_ppo_grad(int obs_dim, int act_dim, const float* const* params, float* con
     if (workspace_bytes < need) return fail(RR_EINVAL, "rr_ppo_grad: workspace smaller than rr_ppo_workspace_size");
     if (((uintptr_t)workspace & 15) != 0) return fail(RR_EINVAL, "rr_ppo_grad: workspace must be 16-B aligned");
     if (!(clip_range >= 0.0f)) return fail(RR_EINVAL, "rr_ppo_grad: clip_range must be >= 0");
-    PolSrc ps;
-    PolGrad pg;
+    PpoLaunch L = {};
+    L.op = 0;
     for (int k = 0; k < 13; ++k) {
         if (!params[k] || !grads[k]) return fail(RR_EINVAL, "rr_ppo_grad: null parameter or gradient tensor");
-        ps.p[k] = params[k];
-        pg.p[k] = grads[k];
+        L.ps.p[k] = params[k];
+        L.pg.p[k] = grads[k];
     }
-    hipStream_t s = (hipStream_t)stream;
-    double* adv_part = (double*)workspace;
-    float* part = (float*)((char*)workspace + 2 * ppo::kAdvPart * sizeof(double));
-    const int nwg = (int)ppo_nwg(batch);
-    auto run = [&](auto obs_c, auto act_c) {
-        constexpr int O = decltype(obs_c)::value, A = decltype(act_c)::value;
-        using PT = ppo::Part<O, A>;
-        using K = ppo::Pack<O, A>;
-        float* pack = part + 2 * (int64_t)nwg * PT::SIZE;  // 16-B aligned: PT::SIZE % 4 == 0
-        hipLaunchKernelGGL((ppo_prep_kernel<O, A>), dim3(ppo::kAdvPart + (2 * K::SIZE + 255) / 256), dim3(256), 0, s,
-                           advantages, idx, batch, adv_part, ps, pack);
-        hipLaunchKernelGGL((ppo_grad_kernel<O, A>), dim3(nwg, 2), dim3(ppo::kThreads), 0, s, obs, actions,
-                           old_log_prob, advantages, returns, idx, batch, clip_range, vf_coef, adv_part, pack, part);
-        hipLaunchKernelGGL((ppo_finish_kernel<O, A>), dim3((PT::SIZE + kFinElems - 1) / kFinElems, 2), dim3(256), 0, s, part, nwg, batch,
-                           ent_coef, ps, pg, stats, nullptr, nullptr);
-    };
-    if (obs_dim == 14) run(std::integral_constant<int, 14>{}, std::integral_constant<int, 3>{});
-    else run(std::integral_constant<int, 7>{}, std::integral_constant<int, 2>{});
-    hipError_t err = hipGetLastError();
+    ppo_carve(L, obs_dim, act_dim, batch, workspace);
+    L.obs = obs;
+    L.actions = actions;
+    L.old_log_prob = old_log_prob;
+    L.advantages = advantages;
+    L.returns = returns;
+    L.idx = idx;
+    L.batch = batch;
+    L.clip = clip_range;
+    L.ent = ent_coef;
+    L.vf = vf_coef;
+    L.stats = stats;
+    const hipError_t err = (hipError_t)rrc_launch_learner(&L, stream);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_ppo_grad: launch");
 }
 
@@ -2693,49 +2750,46 @@ int rr_ppo_update(int obs_dim, int act_dim, float* const* params, float* const* 
         return fail(RR_EINVAL, "rr_ppo_update: next_batch must be in [2, batch]");
     const int na = act_dim, no = obs_dim;
     const int64_t numel[13] = {64 * no, 64, 64 * 64, 64, 64 * no, 64, 64 * 64, 64, 64 * na, na, 64, 1, na};
-    PolSrc ps;
-    PolGrad pg;
-    AdamList a = {};
-    a.n = 13;
+    PpoLaunch L = {};
+    L.op = 1;
+    L.a.n = 13;
     for (int k = 0; k < 13; ++k) {
         if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || !step[k])
             return fail(RR_EINVAL, "rr_ppo_update: null parameter, gradient or optimizer-state tensor");
-        ps.p[k] = params[k];
-        pg.p[k] = grads[k];
-        a.param[k] = params[k];
-        a.grad[k] = grads[k];
-        a.exp_avg[k] = exp_avg[k];
-        a.exp_avg_sq[k] = exp_avg_sq[k];
-        a.step[k] = step[k];
-        a.start[k + 1] = a.start[k] + numel[k];
+        L.ps.p[k] = params[k];
+        L.pg.p[k] = grads[k];
+        L.a.param[k] = params[k];
+        L.a.grad[k] = grads[k];
+        L.a.exp_avg[k] = exp_avg[k];
+        L.a.exp_avg_sq[k] = exp_avg_sq[k];
+        L.a.step[k] = step[k];
+        L.a.start[k + 1] = L.a.start[k] + numel[k];
     }
-    hipStream_t s = (hipStream_t)stream;
-    double* adv_part = (double*)workspace;
-    float* part = (float*)((char*)workspace + 2 * ppo::kAdvPart * sizeof(double));
-    float* normw = (float*)((char*)workspace + (ppo_bytes + 15) / 16 * 16);
-    const int nwg = (int)ppo_nwg(batch);
-    const int nbp = (int)((a.start[13] + kAdamThreads - 1) / kAdamThreads);
-    const AdvNext nx = {advantages, next_idx, next_idx ? next_batch : 0, adv_part};
-    auto run = [&](auto obs_c, auto act_c) {
-        constexpr int O = decltype(obs_c)::value, A = decltype(act_c)::value;
-        using PT = ppo::Part<O, A>;
-        using K = ppo::Pack<O, A>;
-        constexpr int nfin = (PT::SIZE + kFinElems - 1) / kFinElems;
-        float* pack = part + 2 * (int64_t)nwg * PT::SIZE;
-        if (!(flags & RR_PPO_CHAINED))
-            hipLaunchKernelGGL((ppo_prep_kernel<O, A>), dim3(ppo::kAdvPart + (2 * K::SIZE + 255) / 256), dim3(256), 0, s,
-                               advantages, idx, batch, adv_part, ps, pack);
-        hipLaunchKernelGGL((ppo_grad_kernel<O, A>), dim3(nwg, 2), dim3(ppo::kThreads), 0, s, obs, actions,
-                           old_log_prob, advantages, returns, idx, batch, clip_range, vf_coef, adv_part, pack, part);
-        hipLaunchKernelGGL((ppo_finish_kernel<O, A>), dim3(nfin, 2), dim3(256), 0, s, part, nwg, batch, ent_coef, ps, pg,
-                           stats, normw, (const float*)step[0]);
-        hipLaunchKernelGGL((adam_chain_kernel<O, A>), dim3(nbp + (next_idx ? ppo::kAdvPart / 4 : 0)), dim3(kAdamThreads),
-                           0, s, a, (const float*)normw, 2 * nfin, max_grad_norm, lr, (float)beta1, (float)beta2,
-                           (float)(1.0 - beta1), (float)(1.0 - beta2), eps, pack, nx, nbp);
-    };
-    if (obs_dim == 14) run(std::integral_constant<int, 14>{}, std::integral_constant<int, 3>{});
-    else run(std::integral_constant<int, 7>{}, std::integral_constant<int, 2>{});
-    hipError_t err = hipGetLastError();
+    ppo_carve(L, obs_dim, act_dim, batch, workspace);
+    L.normw = (float*)((char*)workspace + (ppo_bytes + 15) / 16 * 16);
+    L.nbp = (int)((L.a.start[13] + kAdamThreads - 1) / kAdamThreads);
+    L.obs = obs;
+    L.actions = actions;
+    L.old_log_prob = old_log_prob;
+    L.advantages = advantages;
+    L.returns = returns;
+    L.idx = idx;
+    L.next_idx = next_idx;
+    L.batch = batch;
+    L.next_batch = next_batch;
+    L.clip = clip_range;
+    L.ent = ent_coef;
+    L.vf = vf_coef;
+    L.max_norm = max_grad_norm;
+    L.lr = lr;
+    L.beta1 = (float)beta1;
+    L.beta2 = (float)beta2;
+    L.w1 = (float)(1.0 - beta1);
+    L.w2 = (float)(1.0 - beta2);
+    L.eps = eps;
+    L.stats = stats;
+    L.flags = flags;
+    const hipError_t err = (hipError_t)rrc_launch_learner(&L, stream);
     return err == hipSuccess ? RR_OK : hip_fail(err, "rr_ppo_update: launch");
 }
 
