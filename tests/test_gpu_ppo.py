@@ -208,15 +208,15 @@ def test_clip_adam_matches_torch():
             assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-12)
 
 
-def _rollout_for_update(n=8192, T=8, seed=4):
+def _rollout_for_update(n=8192, T=8, seed=4, model=6):
     import torch
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
     from rl_rocket_amd.rollout import DeviceRollout, MlpActorCritic
 
-    env = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=30, **ENV_CONFIG_6DOF)
+    env = RocketBatch(n, model=model, device="cuda:0", max_episode_steps=30, **(ENV_CONFIG_6DOF if model == 6 else {}))
     torch.manual_seed(11)
-    pol = MlpActorCritic(14, 3).cuda()
+    pol = MlpActorCritic(env.state_dim, env.action_dim).cuda()
     ro = DeviceRollout(env, pol, n_steps=T, seed=seed)
     ro.collect()
     torch.cuda.synchronize()
@@ -308,7 +308,8 @@ def test_rollout_and_learner_forwards_agree():
     env.close()
 
 
-def test_ppo_update_chain_carries_what_a_fresh_prep_computes():
+@pytest.mark.parametrize("model", [6, 3])
+def test_ppo_update_chain_carries_what_a_fresh_prep_computes(model):
     """rr_ppo_update chained (each call's optimizer launch repacks the towers from the updated
     parameters — the inverse of the pack — and sums the next minibatch's advantage statistics)
     against the same calls each packing and summing for itself: after 2 epochs x 4 minibatches
@@ -318,7 +319,7 @@ def test_ppo_update_chain_carries_what_a_fresh_prep_computes():
     import torch
     from rl_rocket_amd.rollout import ClipAdam, PPOGrad, PPOUpdate
 
-    env, pol, ro = _rollout_for_update()
+    env, pol, ro = _rollout_for_update(model=model)
     n = ro.n_steps * ro.env.num_envs
     bs = 16384
     pols = [copy.deepcopy(pol) for _ in range(3)]
