@@ -827,6 +827,7 @@ class GraphedPPOUpdate:
         self.ret = ro.returns.reshape(n)
         self.coef = (clip_range, ent_coef, vf_coef, max_grad_norm)
         self.perm = torch.arange(n, device=dev)  # refilled per epoch; minibatch k = perm[k bs : (k + 1) bs]
+        self._perm_bufs = self._perm_stream = None  # update(): the next epoch's permutation, drawn aside
         self.n_mb = n // batch_size
         params = list(policy.parameters())
         # state to restore after the warm-up steps (in place: the graph keeps these tensors)
@@ -914,11 +915,32 @@ class GraphedPPOUpdate:
 
     def update(self, n_epochs=10, generator=None):
         """n_epochs passes over the rollout in shuffled minibatches (ppo_update's order:
-        one torch.randperm per epoch)."""
+        one torch.randperm per epoch).
+
+        Each later epoch's permutation is drawn on a side stream while the previous epoch's graph
+        replays: torch's randperm is a ~0.25 ms chain of small sort launches at 1 M rows, and the
+        learner's kernels leave most of each SIMD's wave slots free. The draws are issued in the
+        same order from the same generator, so the permutations are the sequential loop's."""
         for o in (self._adam, self._update):
             if o is not None:
                 o.sync_lr()  # the graph reads lr from the device: follow param_groups[0]["lr"]
-        for _ in range(n_epochs):
-            self.perm.copy_(torch.randperm(self.n, device=self.obs.device, generator=generator))
+        dev = self.obs.device
+        main = torch.cuda.current_stream(dev)
+        if self._perm_bufs is None:
+            self._perm_bufs = (torch.empty_like(self.perm), torch.empty_like(self.perm))
+            self._perm_stream = torch.cuda.Stream(dev)
+        bufs, side = self._perm_bufs, self._perm_stream
+        torch.randperm(self.n, out=bufs[0], generator=generator)
+        ready = None
+        for e in range(n_epochs):
+            cur = bufs[e % 2]
+            if ready is not None:
+                main.wait_event(ready)
+            self.perm.copy_(cur)
+            if e + 1 < n_epochs:
+                side.wait_stream(main)  # the other buffer's last reader (the previous copy) is done
+                with torch.cuda.stream(side):
+                    torch.randperm(self.n, out=bufs[(e + 1) % 2], generator=generator)
+                    ready = side.record_event()
             self.graph.replay()
         return {k: float(v) for k, v in self.stats.items()}

@@ -113,6 +113,41 @@ def test_ppo_grad_overwrites_and_is_deterministic():
         assert torch.equal(a, t.grad)
 
 
+def test_graphed_update_draws_the_sequential_permutations():
+    """GraphedPPOUpdate.update draws each later epoch's permutation on a side stream while the
+    previous epoch replays: every epoch still sees exactly the permutation a sequential loop of
+    torch.randperm calls on the same generator gives (n = 65 536: torch's on-device sort path)."""
+    import torch
+    from rl_rocket_amd.batch import RocketBatch
+    from rl_rocket_amd.params import ENV_CONFIG_6DOF
+    from rl_rocket_amd.rollout import DeviceRollout, GraphedPPOUpdate, MlpActorCritic
+
+    n, T, bs = 8192, 8, 16384
+    env = RocketBatch(n, model=6, device="cuda:0", max_episode_steps=30, **ENV_CONFIG_6DOF)
+    torch.manual_seed(12)
+    pol = MlpActorCritic(14, 3).cuda()
+    ro = DeviceRollout(env, pol, n_steps=T, seed=4)
+    ro.collect()
+    opt = torch.optim.Adam(pol.parameters(), lr=1e-3, capturable=True)
+    g = GraphedPPOUpdate(pol, opt, ro, batch_size=bs, fused=True)
+    seen = []
+
+    class _Record:  # stands in for the epoch's graph: what the replay would read
+        def replay(self):
+            seen.append(g.perm.clone())
+
+    g.graph = _Record()
+    g.update(n_epochs=5, generator=torch.Generator("cuda:0").manual_seed(13))
+    gen = torch.Generator("cuda:0").manual_seed(13)
+    want = [torch.randperm(n * T, device="cuda:0", generator=gen) for _ in range(5)]
+    torch.cuda.synchronize()
+    assert len(seen) == 5
+    for e, (a, b) in enumerate(zip(seen, want)):
+        assert torch.equal(a, b), e
+    assert len({tuple(a[:8].tolist()) for a in seen}) == 5  # five different draws
+    env.close()
+
+
 def test_fused_update_graphed_equals_eager_and_tracks_autograd():
     """ppo_update(fused=True) and GraphedPPOUpdate(fused=True) from the same state and shuffling:
     bitwise equal (same launches in the same order); and against the PyTorch-autograd ppo_update,
