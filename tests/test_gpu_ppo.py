@@ -113,6 +113,28 @@ def test_ppo_grad_overwrites_and_is_deterministic():
         assert torch.equal(a, t.grad)
 
 
+def test_epoch_perms_are_the_sequential_draws():
+    """ppo_update(fused=True)'s permutations, each later epoch's drawn on a side stream: the same
+    tensors as a sequential loop of torch.randperm on the same generator, each one ready on the
+    caller's stream when it is yielded (a slow consumer in between changes nothing)."""
+    import torch
+    from rl_rocket_amd.rollout import _epoch_perms
+
+    n = 1 << 17
+    seen = []
+    x = torch.randn(4096, 4096, device="cuda:0")
+    for p in _epoch_perms(n, 4, torch.device("cuda:0"), torch.Generator("cuda:0").manual_seed(21)):
+        x = x @ x.T * 1e-3  # keep the current stream busy while the next draw runs aside
+        seen.append(p.clone())
+    gen = torch.Generator("cuda:0").manual_seed(21)
+    want = [torch.randperm(n, device="cuda:0", generator=gen) for _ in range(4)]
+    torch.cuda.synchronize()
+    assert len(seen) == 4
+    for e, (a, b) in enumerate(zip(seen, want)):
+        assert torch.equal(a, b), e
+    assert list(_epoch_perms(n, 0, torch.device("cuda:0"))) == []
+
+
 def test_graphed_update_draws_the_sequential_permutations():
     """GraphedPPOUpdate.update draws each later epoch's permutation on a side stream while the
     previous epoch replays: every epoch still sees exactly the permutation a sequential loop of
