@@ -2764,10 +2764,11 @@ int rr_ppo_update(int obs_dim, int act_dim, float* const* params, float* const* 
         L.a.exp_avg_sq[k] = exp_avg_sq[k];
         L.a.step[k] = step[k];
         L.a.start[k + 1] = L.a.start[k] + numel[k];
+        L.a.wstart[k + 1] = L.a.wstart[k] + (numel[k] + kWave - 1) / kWave * kWave;
     }
     ppo_carve(L, obs_dim, act_dim, batch, workspace);
     L.normw = (float*)((char*)workspace + (ppo_bytes + 15) / 16 * 16);
-    L.nbp = (int)((L.a.start[13] + kAdamThreads - 1) / kAdamThreads);
+    L.nbp = (int)((L.a.wstart[13] + kAdamThreads - 1) / kAdamThreads);
     L.obs = obs;
     L.actions = actions;
     L.old_log_prob = old_log_prob;
