@@ -2,7 +2,7 @@
 # The learner's kernels in the collect TU (MFMA accumulators in VGPRs): learner / rollout tests,
 # bitwise vs the previous build, phase clocks, rollout-bench PPO legs of both builds interleaved
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" || exit 2
-OUT="$R/gpurun_out/r06ah"; mkdir -p "$OUT"
+OUT="$R/gpurun_out/r06ai"; mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ppo.py tests/test_gpu_rollout.py -x -v --timeout 300 --timeout-method thread -m gpu > "$OUT/tests.log" 2>&1
 rc=$?; tail -1 "$OUT/tests.log"; [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" "$OUT/tests.log" | head -30; exit $rc; }
 timeout -k 10 300 python tools/ppo_grad_bitwise.py --libs tree,tools/ab/lib_prev.so --out "$OUT/bitwise.json" > "$OUT/bitwise.log" 2>&1
