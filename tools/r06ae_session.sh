@@ -2,7 +2,7 @@
 # The next epoch's permutation drawn on a side stream during the replay: learner / rollout tests,
 # then the rollout bench's PPO legs twice
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" || exit 2
-OUT="$R/gpurun_out/r06ag"; mkdir -p "$OUT"
+OUT="$R/gpurun_out/r06an"; mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ppo.py tests/test_gpu_rollout.py -x -v --timeout 300 --timeout-method thread -m gpu > "$OUT/tests.log" 2>&1
 rc=$?; tail -1 "$OUT/tests.log"; [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" "$OUT/tests.log" | head -30; exit $rc; }
 for rep in 1 2; do
