@@ -432,6 +432,7 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
 
         def train_loop():
             for _ in range(iters):
+                gu.prepare()  # the first epoch's permutation drawn beside the collect
                 g.replay()
                 gu.update(n_epochs=10)
 
@@ -446,7 +447,8 @@ def bench_rollout(args, dev, n, model, kw, dist=None, rank=0, world=1):
                  "ms_per_iteration": tt / iters * 1e3,
                  "what": "one training iteration = one collect (n_steps x N env-steps, one hipGraph) + 10 PPO epochs "
                          "of graphed minibatch updates (SB3 1.6 defaults: n_epochs 10), batch_size N, the whole "
-                         "minibatch step (loss + backward + clip + Adam) by rr_ppo_update, chained"}
+                         "minibatch step (loss + backward + clip + Adam) by rr_ppo_update, chained; each epoch's "
+                         "permutation drawn on a side stream beside the collect / the previous epoch"}
     env.close()
     # roofline of the collect kernel (rollout_step_kernel<..., MULTI = true>): the policy towers
     # are the contraction (fp32 MFMA in the default precision), so the bound is the MFMA peak;

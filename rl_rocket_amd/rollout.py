@@ -850,6 +850,7 @@ class GraphedPPOUpdate:
         self.coef = (clip_range, ent_coef, vf_coef, max_grad_norm)
         self.perm = torch.arange(n, device=dev)  # refilled per epoch; minibatch k = perm[k bs : (k + 1) bs]
         self._perm_bufs = self._perm_stream = None  # update(): the next epoch's permutation, drawn aside
+        self._first = None  # prepare(): the event of the next update's first draw
         self.n_mb = n // batch_size
         params = list(policy.parameters())
         # state to restore after the warm-up steps (in place: the graph keeps these tensors)
@@ -935,6 +936,24 @@ class GraphedPPOUpdate:
         self.optimizer.step()
         return {"policy_loss": pg.detach(), "value_loss": vf.detach(), "entropy": -ent.detach()}
 
+    def _perm_streams(self):
+        dev = self.obs.device
+        if self._perm_bufs is None:
+            self._perm_bufs = (torch.empty_like(self.perm), torch.empty_like(self.perm))
+            self._perm_stream = torch.cuda.Stream(dev)
+        return torch.cuda.current_stream(dev), self._perm_bufs, self._perm_stream
+
+    def prepare(self, generator=None):
+        """Draw the next ``update``'s first-epoch permutation now, on the side stream: called
+        before the rollout collect, the draw runs beside it instead of ahead of the first
+        epoch. It is the draw ``update`` would make first; pass ``update`` the same generator
+        and draw nothing else from it in between."""
+        main, bufs, side = self._perm_streams()
+        side.wait_stream(main)  # the previous update's readers of bufs[0] are done
+        with torch.cuda.stream(side):
+            torch.randperm(self.n, out=bufs[0], generator=generator)
+            self._first = side.record_event()
+
     def update(self, n_epochs=10, generator=None):
         """n_epochs passes over the rollout in shuffled minibatches (ppo_update's order:
         one torch.randperm per epoch).
@@ -942,18 +961,15 @@ class GraphedPPOUpdate:
         Each later epoch's permutation is drawn on a side stream while the previous epoch's graph
         replays: torch's randperm is a ~0.25 ms chain of small sort launches at 1 M rows, and the
         learner's kernels leave most of each SIMD's wave slots free. The draws are issued in the
-        same order from the same generator, so the permutations are the sequential loop's."""
+        same order from the same generator, so the permutations are the sequential loop's. After
+        ``prepare`` the first epoch uses the permutation drawn there."""
         for o in (self._adam, self._update):
             if o is not None:
                 o.sync_lr()  # the graph reads lr from the device: follow param_groups[0]["lr"]
-        dev = self.obs.device
-        main = torch.cuda.current_stream(dev)
-        if self._perm_bufs is None:
-            self._perm_bufs = (torch.empty_like(self.perm), torch.empty_like(self.perm))
-            self._perm_stream = torch.cuda.Stream(dev)
-        bufs, side = self._perm_bufs, self._perm_stream
-        torch.randperm(self.n, out=bufs[0], generator=generator)
-        ready = None
+        main, bufs, side = self._perm_streams()
+        ready, self._first = self._first, None
+        if ready is None:  # no prepare(): the first epoch's draw in line
+            torch.randperm(self.n, out=bufs[0], generator=generator)
         for e in range(n_epochs):
             cur = bufs[e % 2]
             if ready is not None:

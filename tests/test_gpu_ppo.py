@@ -135,10 +135,12 @@ def test_epoch_perms_are_the_sequential_draws():
     assert list(_epoch_perms(n, 0, torch.device("cuda:0"))) == []
 
 
-def test_graphed_update_draws_the_sequential_permutations():
+@pytest.mark.parametrize("prepared", [False, True])
+def test_graphed_update_draws_the_sequential_permutations(prepared):
     """GraphedPPOUpdate.update draws each later epoch's permutation on a side stream while the
-    previous epoch replays: every epoch still sees exactly the permutation a sequential loop of
-    torch.randperm calls on the same generator gives (n = 65 536: torch's on-device sort path)."""
+    previous epoch replays (and, after prepare(), the first one before the update): every epoch
+    still sees exactly the permutation a sequential loop of torch.randperm calls on the same
+    generator gives (n = 65 536: torch's on-device sort path)."""
     import torch
     from rl_rocket_amd.batch import RocketBatch
     from rl_rocket_amd.params import ENV_CONFIG_6DOF
@@ -159,7 +161,11 @@ def test_graphed_update_draws_the_sequential_permutations():
             seen.append(g.perm.clone())
 
     g.graph = _Record()
-    g.update(n_epochs=5, generator=torch.Generator("cuda:0").manual_seed(13))
+    gen0 = torch.Generator("cuda:0").manual_seed(13)
+    if prepared:
+        g.prepare(gen0)
+        ro.collect()  # what prepare() is for: the draw runs beside the collect
+    g.update(n_epochs=5, generator=gen0)
     gen = torch.Generator("cuda:0").manual_seed(13)
     want = [torch.randperm(n * T, device="cuda:0", generator=gen) for _ in range(5)]
     torch.cuda.synchronize()
